@@ -1,0 +1,259 @@
+#!/usr/bin/env python3
+"""framesum benchmark — BASELINE.json metric on MI355X.
+
+A "step" = one pass of the hot path (fused CRC-32 + IPv4 + TCP/UDP checksum +
+RecvEth verdict) over one batch of synthetic frames already resident in HBM.
+Default workload (BASELINE configs[1], C2): 65,536 x 1500-byte TCP frames per
+GPU; --config c3 runs the mixed 64/576/1500/9000 batch. NB >= 4 distinct
+batches (> 256 MiB in total) are rotated so the 256 MiB Infinity Cache cannot
+serve them. Multi-GPU (torchrun, one process per GPU, RCCL = torch "nccl"):
+every rank digests its own shard (weak scaling, frame i of the global batch
+on rank i mod N) and the per-frame digests + verdicts are gathered to rank 0
+over RCCL, pipelined one step behind the kernels; no other collective.
+
+Prints ONE JSON line on rank 0 (see the contract in DESIGN.md §5).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s)
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", choices=["c2", "c3"], default="c2")
+    p.add_argument("--frames", type=int, default=65536, help="frames per GPU per step")
+    p.add_argument("--batches", type=int, default=4, help="distinct resident batches rotated")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
+    p.add_argument("--cpu-threads", type=int, default=1)
+    p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather (N>1 diagnostics)")
+    return p.parse_args()
+
+
+def make_batch(cfg: str, n: int, seed: int):
+    from seqs_amd import synth
+
+    if cfg == "c2":
+        return synth.uniform_batch(n, 1500, seed=seed)
+    return synth.mixed_batch(n, seed=seed)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg: str, seconds: float, threads: int):
+    """The C oracle (scalar restatement of eth/crc.go + headers.go + RecvEth gates, zlib
+    CRC-32) timed on a bounded C1-style sample: 4,096 frames of the same workload."""
+    from oracle import coracle
+
+    coracle.load()
+    buf, off, ln = make_batch(cfg, 4096, seed=101)
+    nbytes = int(ln.astype(np.int64).sum())
+    coracle.digest_batch(buf, off, ln, mtu=0, nthreads=threads)  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        coracle.digest_batch(buf, off, ln, mtu=0, nthreads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and reps >= 3:
+            break
+    gibs = nbytes * reps / el / GIB
+    return {
+        "value": round(gibs, 4),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{reps} x C1-style batch of 4096 {'1500-B TCP' if cfg == 'c2' else 'mixed'} frames "
+                  f"({nbytes} B) through oracle/framesum_oracle.c (CRC791 loop -O2 -fno-tree-vectorize + zlib "
+                  f"crc32), {el:.1f} s on {cpu_model()}",
+    }
+
+
+def load_pmc_traffic(cfg: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world == 1:
+        # started without torchrun: run ourselves under it as a child process
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29511"),
+               os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.run(cmd).returncode)
+
+    import torch
+    import torch.distributed as dist
+
+    from seqs_amd import Engine
+
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    n = args.frames
+    engine = Engine(local)
+    batches = []
+    for b in range(max(1, args.batches)):
+        buf, off, ln = make_batch(args.config, n, seed=1 + 1000 * rank + b)
+        batches.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev),
+                        torch.from_numpy(ln).to(dev)))
+    bytes_per_batch = int(ln.astype(np.int64).sum())
+    resident = sum(int(x[0].numel()) for x in batches)
+    nb = len(batches)
+    outs = [torch.empty((n, 2), dtype=torch.int32, device=dev) for _ in range(2)]
+    stats = [torch.empty((n,), dtype=torch.uint8, device=dev) for _ in range(2)]
+    gather = world > 1 and not args.no_gather
+    if gather:
+        g_out = [[torch.empty((n, 2), dtype=torch.int32, device=dev) for _ in range(world)] for _ in range(2)]
+        g_st = [[torch.empty((n,), dtype=torch.uint8, device=dev) for _ in range(world)] for _ in range(2)]
+    stream = torch.cuda.current_stream(dev)
+
+    pending = []
+
+    def step(i: int, ev=None):
+        fb, fo, fl = batches[i % nb]
+        k = i & 1
+        if ev is not None:
+            ev[0].record(stream)
+        engine.digest_device(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        if gather:
+            # wait for the gather that used this output slot two steps ago, then gather this step's
+            while len(pending) >= 2:
+                for w in pending.pop(0):
+                    w.wait()
+            hs = [dist.gather(outs[k], g_out[k] if rank == 0 else None, dst=0, async_op=True),
+                  dist.gather(stats[k], g_st[k] if rank == 0 else None, dst=0, async_op=True)]
+            pending.append(hs)
+
+    def drain():
+        while pending:
+            for w in pending.pop(0):
+                w.wait()
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
+    torch.cuda.synchronize()
+
+    # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- kernel-only timing with HIP events on the launch stream (roofline.achieved)
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    saved_gather = gather
+    gather = False
+    for i in range(args.steps):
+        step(i, kev[i])
+    torch.cuda.synchronize()
+    gather = saved_gather
+    kms = sorted(a.elapsed_time(b) for a, b in kev)
+    k_avg_ms = sum(kms) / len(kms)
+    k_med_ms = kms[len(kms) // 2]
+
+    total_bytes = bytes_per_batch * args.steps * world
+    value = total_bytes / elapsed / GIB
+    achieved_gbs = bytes_per_batch / (k_avg_ms * 1e-3) / 1e9
+    traffic = load_pmc_traffic(args.config)
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(args.config, args.cpu_seconds, args.cpu_threads)
+        result = {
+            "metric": "GiB/s device-resident CRC-32+Internet-csum over batched MTU frames; % HBM peak",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic: {nb} distinct resident batches ({resident / 1e6:.0f} MB) of valid frames, rotated",
+            "config": {
+                "workload": ("C2: 65536 x 1500-B TCP frames per GPU (BASELINE configs[1])" if args.config == "c2"
+                             else "C3: 65536 mixed 64/576/1500/9000-B TCP/UDP frames per GPU (BASELINE configs[2])")
+                if n == 65536 else f"{args.config} with {n} frames per GPU",
+                "frames_per_gpu": n,
+                "bytes_per_gpu_step": bytes_per_batch,
+                "global_batch_frames": n * world,
+                "parallelism": f"frames sharded round-robin over {world} GPU(s); RCCL gather of digests to rank 0"
+                if world > 1 else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbs, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "digest_kernel",
+                "kernel_avg_us": round(k_avg_ms * 1e3, 3),
+                "kernel_median_us": round(k_med_ms * 1e3, 3),
+                "algorithmic_bytes_per_launch": bytes_per_batch,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    engine.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+/*
+ * framesum — MI355X-native batched frame-checksum engine (C ABI).
+ *
+ * Drop-in boundary for the soypat/seqs per-frame checksum path. The Go
+ * reference computes, for every frame through stacks.PortStack.RecvEth, the
+ * RFC 791/1071 one's-complement checksums of eth/crc.go + eth/headers.go one
+ * frame per synchronous call. This ABI replaces those per-frame calls with
+ * one batched, device-resident call; the per-frame Go functions stay as they
+ * are. Plain pointers and sizes only: no HIP, torch or C++
+ * types cross the boundary, so cgo / ctypes / JNI can bind it directly
+ * (INTEGRATION.md shows the bindings).
+ *
+ * Replaced reference interfaces (paths relative to the soypat/seqs root):
+ *   fs_digest.l4_csum + fs verdict  <- stacks/portstack.go:239-244 (UDP) and
+ *        :301-308 (TCP): `gotsum := uhdr.CalculateChecksumIPv4(&ihdr, payload)`
+ *        / `thdr.CalculateChecksumIPv4(&ihdr, tcpOptions, payload)` and the
+ *        compare that yields ErrChecksumTCPorUDP (portstack.go:132), together
+ *        with the RecvEth gates that choose the L4 range (:167-214, :226-237,
+ *        :285-299) and the verdict errors (:120-142).
+ *   fs_digest.ip_csum               <- eth/headers.go:333-340
+ *        (*IPv4Header).CalculateChecksum() applied to frame[14:34].
+ *   the CRC791 arithmetic itself    <- eth/crc.go:13-84 (Write/AddUint16/
+ *        AddUint32/AddUint8/Sum16/Reset), evaluated on the GPU.
+ *   fs_digest.crc32                 <- NEW: IEEE 802.3 CRC-32 (Ethernet FCS)
+ *        over frame[0:len). The reference has no CRC-32.
+ *
+ * Conventions (mirroring the reference's): pure functions over caller-owned
+ * buffers, no retention after the call's stream work completes; malformed
+ * frames are reported per frame in `status` (the RecvEth error class), never
+ * as a call failure. Errors of the call itself are negative fs_status codes
+ * (no exceptions cross the ABI); fs_last_error() gives the message.
+ * Threading: one fs_ctx per host thread (a context is not internally locked).
+ */
+#ifndef FRAMESUM_H
+#define FRAMESUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRAMESUM_ABI_VERSION 1u
+
+typedef int32_t fs_status;
+#define FS_SUCCESS 0
+#define FS_E_INVALID (-1)   /* bad argument (null pointer, n too large, ...) */
+#define FS_E_HIP (-2)       /* HIP runtime error (message in fs_last_error) */
+#define FS_E_NOMEM (-3)     /* device or pinned-host allocation failed */
+#define FS_E_NODEVICE (-4)  /* no such device / device is not gfx950 */
+
+/* Per-frame verdict written to `status` (stacks/portstack.go:120-142). The
+ * stack model: MTU `mtu` (0 disables both MTU gates so jumbo frames can be
+ * evaluated; the reference caps MTU at 2048, portstack.go:17,46-48), address
+ * filters off (MAC :185-186 and IP destination :209-210 are socket-layer
+ * policy, not checksum inputs), one UDP and one TCP port open. */
+enum fs_verdict {
+    FS_OK = 0,                          /* L4 checksum verified (RecvEth continues) */
+    FS_ERR_PACKET_SMOL = 1,             /* errPacketSmol */
+    FS_ERR_EXCEEDS_MTU = 2,             /* errPacketExceedsMTU */
+    FS_IGNORED_NOT_IPV4 = 3,            /* RecvEth returns nil: not IPv4/ARP */
+    FS_ARP = 4,                         /* ARP frame (no checksum) */
+    FS_ERR_IP_VERSION = 5,              /* errIPVersion */
+    FS_ERR_INVALID_IHL = 6,             /* errInvalidIHL */
+    FS_ERR_BAD_IP_TOTAL_LEN_OR_IHL = 7, /* errBadIPTotalLenOrIHL */
+    FS_ERR_UNKNOWN_IP_PROTO = 8,        /* errUnknownIPProto */
+    FS_ERR_TOO_SHORT_TCP_OR_UDP = 9,    /* errTooShortTCPOrUDP */
+    FS_ERR_ZERO_PORT = 10,              /* errZeroPort */
+    FS_ERR_BAD_UDP_LENGTH = 11,         /* errBadUDPLength */
+    FS_ERR_BAD_TCP_OFFSET = 12,         /* errBadTCPOffset */
+    FS_ERR_CHECKSUM = 13                /* ErrChecksumTCPorUDP */
+};
+
+/* 8-byte per-frame digest. crc32: IEEE CRC-32 of frame[0:len).
+ * ip_csum: IPv4Header.CalculateChecksum() of frame[14:34] (0 if len < 34).
+ * l4_csum: the TCP/UDP checksum RecvEth computes (`gotsum`), 0 when the frame
+ * is rejected before the compare (status not FS_OK / FS_ERR_CHECKSUM). */
+typedef struct fs_digest {
+    uint32_t crc32;
+    uint16_t ip_csum;
+    uint16_t l4_csum;
+} fs_digest;
+
+typedef struct fs_ctx fs_ctx;
+
+/* Library / device queries. */
+uint32_t fs_abi_version(void);
+int fs_device_count(void);
+
+/* Context: owns the device copy of the CRC shift tables, staging buffers and
+ * an internal stream for the host-staged entry point. */
+fs_status fs_ctx_create(int device, fs_ctx** out);
+fs_status fs_ctx_destroy(fs_ctx* ctx);
+/* Message for the last failing call on `ctx` (or of fs_ctx_create when ctx is NULL). */
+const char* fs_last_error(const fs_ctx* ctx);
+
+/* Batched digest, device-resident. All pointers are DEVICE pointers.
+ *   frame i = frames[offsets[i] : offsets[i] + lengths[i]]  (any byte alignment,
+ *   frames may overlap or be sparse; the engine may read up to 3 bytes past a
+ *   frame's end, i.e. `frames` must be readable up to round_up(end, 4)).
+ *   out[i] receives the digest; status (nullable) receives the fs_verdict.
+ * Asynchronous on `stream` (a hipStream_t; NULL = the null stream). */
+fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths,
+                          uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status, void* stream);
+
+/* Same computation from/to HOST memory (the NIC / loopback buffer handed to
+ * RecvEth): stages H2D, runs the kernel and copies D2H on the context's
+ * stream, returning when the results are in `out`/`status`. Pinned memory
+ * (fs_host_alloc) gives full PCIe rate; pageable memory works. */
+fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
+                               const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status);
+
+/* Pinned host memory helpers for fs_digest_batch_host callers. */
+fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out);
+fs_status fs_host_free(fs_ctx* ctx, void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRAMESUM_H */

@@ -1,0 +1,238 @@
+"""Host-side binding of the framesum C ABI (include/framesum.h).
+
+This is the Python mirror of the reference's batch surface: `digest_batch`
+plays the role of running `stacks.PortStack.RecvEth`'s checksum gates plus
+`eth.(*IPv4Header).CalculateChecksum` / `(*UDPHeader|*TCPHeader).CalculateChecksumIPv4`
+(eth/headers.go:333, :382, :510) over many frames at once, and
+`recv_eth_batch` returns the per-frame RecvEth error class
+(stacks/portstack.go:120-142). All digests are computed by the gfx950 kernel
+in seqs_amd/lib/libframesum.so; there is no CPU fallback — if the library or a
+gfx950 device is missing, the calls raise.
+
+torch is used only as device-memory / stream plumbing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libframesum.so")
+
+FS_SUCCESS = 0
+FS_E_INVALID = -1
+FS_E_HIP = -2
+FS_E_NOMEM = -3
+FS_E_NODEVICE = -4
+
+# fs_verdict (include/framesum.h) — RecvEth error classes (stacks/portstack.go:120-142).
+VERDICTS = {
+    0: "OK",
+    1: "errPacketSmol",
+    2: "errPacketExceedsMTU",
+    3: "ignored (not IPv4/ARP)",
+    4: "ARP",
+    5: "errIPVersion",
+    6: "errInvalidIHL",
+    7: "errBadIPTotalLenOrIHL",
+    8: "errUnknownIPProto",
+    9: "errTooShortTCPOrUDP",
+    10: "errZeroPort",
+    11: "errBadUDPLength",
+    12: "errBadTCPOffset",
+    13: "ErrChecksumTCPorUDP",
+}
+
+# Every symbol include/framesum.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "fs_abi_version",
+    "fs_device_count",
+    "fs_ctx_create",
+    "fs_ctx_destroy",
+    "fs_last_error",
+    "fs_digest_batch",
+    "fs_digest_batch_host",
+    "fs_host_alloc",
+    "fs_host_free",
+)
+
+DIGEST_DTYPE = np.dtype([("crc32", "<u4"), ("ip_csum", "<u2"), ("l4_csum", "<u2")])
+
+
+class FramesumError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libframesum.so (raises if it was not built: no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise FramesumError(f"{_LIB_PATH} is missing — run __graft_entry__.build() (or make -C seqs_amd/csrc)")
+    lib = ctypes.CDLL(_LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    lib.fs_abi_version.restype = u32
+    lib.fs_abi_version.argtypes = []
+    lib.fs_device_count.restype = ctypes.c_int
+    lib.fs_device_count.argtypes = []
+    lib.fs_ctx_create.restype = i32
+    lib.fs_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    lib.fs_ctx_destroy.restype = i32
+    lib.fs_ctx_destroy.argtypes = [vp]
+    lib.fs_last_error.restype = ctypes.c_char_p
+    lib.fs_last_error.argtypes = [vp]
+    lib.fs_digest_batch.restype = i32
+    lib.fs_digest_batch.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp]
+    lib.fs_digest_batch_host.restype = i32
+    lib.fs_digest_batch_host.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp, vp]
+    lib.fs_host_alloc.restype = i32
+    lib.fs_host_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
+    lib.fs_host_free.restype = i32
+    lib.fs_host_free.argtypes = [vp, vp]
+    _lib = lib
+    return lib
+
+
+@dataclass
+class Digest:
+    """One frame's results (fs_digest + verdict)."""
+
+    crc32: int
+    ip_csum: int
+    l4_csum: int
+    verdict: int
+
+    @property
+    def err(self) -> Optional[str]:
+        return None if self.verdict == 0 else VERDICTS.get(self.verdict, f"verdict {self.verdict}")
+
+
+class Engine:
+    """One framesum context on one GPU (fs_ctx). Not thread-safe, like the C ctx."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self.device = device
+        ctx = ctypes.c_void_p()
+        st = self.lib.fs_ctx_create(device, ctypes.byref(ctx))
+        if st != FS_SUCCESS:
+            raise FramesumError(f"fs_ctx_create({device}) failed ({st}): {self.lib.fs_last_error(None).decode()}")
+        self._ctx = ctx
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self.lib.fs_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int, what: str) -> None:
+        if st != FS_SUCCESS:
+            raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
+
+    # ---- device-resident path (torch tensors as device memory) -------------
+    def digest_device(self, frames, offsets, lengths, mtu: int = 0, out=None, status=None, stream=None):
+        """Device-resident batch digest.
+
+        frames: uint8 CUDA tensor; offsets: int64 CUDA tensor; lengths: int32
+        CUDA tensor. Returns (out, status): out is an int32 tensor of shape
+        (n, 2) holding the raw fs_digest words ([:,0] = crc32 bits,
+        [:,1] = ip_csum | l4_csum << 16), status a uint8 tensor. Asynchronous
+        on `stream` (default: torch's current stream).
+        """
+        import torch
+
+        n = int(lengths.numel())
+        assert frames.is_cuda and offsets.is_cuda and lengths.is_cuda, "device-resident path needs CUDA tensors"
+        assert frames.dtype == torch.uint8 and offsets.dtype == torch.int64 and lengths.dtype == torch.int32
+        assert offsets.numel() == n and frames.is_contiguous() and offsets.is_contiguous() and lengths.is_contiguous()
+        if out is None:
+            out = torch.empty((n, 2), dtype=torch.int32, device=frames.device)
+        if status is None:
+            status = torch.empty((n,), dtype=torch.uint8, device=frames.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.device)
+        st = self.lib.fs_digest_batch(
+            self._ctx,
+            ctypes.c_void_p(frames.data_ptr()),
+            ctypes.c_void_p(offsets.data_ptr()),
+            ctypes.c_void_p(lengths.data_ptr()),
+            n,
+            mtu,
+            ctypes.c_void_p(out.data_ptr()),
+            ctypes.c_void_p(status.data_ptr()),
+            ctypes.c_void_p(stream.cuda_stream),
+        )
+        self._check(st, "fs_digest_batch")
+        return out, status
+
+    # ---- host-staged path (numpy in, numpy out) -----------------------------
+    def digest_host(self, frames: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, mtu: int = 0):
+        """Host buffers in, host results out (fs_digest_batch_host). Returns (digests, status)."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        n = int(lengths.size)
+        out = np.zeros(n, dtype=DIGEST_DTYPE)
+        status = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return out, status
+        st = self.lib.fs_digest_batch_host(
+            self._ctx,
+            frames.ctypes.data_as(ctypes.c_void_p),
+            frames.nbytes,
+            offsets.ctypes.data_as(ctypes.c_void_p),
+            lengths.ctypes.data_as(ctypes.c_void_p),
+            n,
+            mtu,
+            out.ctypes.data_as(ctypes.c_void_p),
+            status.ctypes.data_as(ctypes.c_void_p),
+        )
+        self._check(st, "fs_digest_batch_host")
+        return out, status
+
+    # ---- reference-shaped surface -------------------------------------------
+    def digest_batch(self, frames: Sequence[bytes], mtu: int = 0) -> list[Digest]:
+        """Batched equivalent of RecvEth's checksum work for each frame (host lists)."""
+        buf, offsets, lengths = pack_frames(frames)
+        dig, st = self.digest_host(buf, offsets, lengths, mtu)
+        return [Digest(int(d["crc32"]), int(d["ip_csum"]), int(d["l4_csum"]), int(s)) for d, s in zip(dig, st)]
+
+    def recv_eth_batch(self, frames: Sequence[bytes], mtu: int = 0) -> list[Optional[str]]:
+        """Per-frame RecvEth error class (None = checksum OK), like RecvEth's return."""
+        return [d.err for d in self.digest_batch(frames, mtu)]
+
+
+def pack_frames(frames: Sequence[bytes], align: int = 4):
+    """Pack a list of frames into one buffer (each frame at an `align`-aligned offset)."""
+    lengths = np.fromiter((len(f) for f in frames), dtype=np.uint32, count=len(frames))
+    step = (lengths.astype(np.uint64) + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
+    offsets = np.zeros(len(frames), dtype=np.uint64)
+    if len(frames) > 1:
+        offsets[1:] = np.cumsum(step[:-1])
+    total = int(offsets[-1] + step[-1]) if len(frames) else 0
+    buf = np.zeros(total + 16, dtype=np.uint8)
+    for f, o in zip(frames, offsets):
+        buf[int(o) : int(o) + len(f)] = np.frombuffer(f, dtype=np.uint8)
+    return buf, offsets, lengths
+
+
+def split_digests(out_words: np.ndarray):
+    """(n,2) int32 raw digest words -> (crc32 u32, ip_csum u16, l4_csum u16) numpy arrays."""
+    w = np.ascontiguousarray(out_words).view(np.uint32).reshape(-1, 2)
+    return w[:, 0].copy(), (w[:, 1] & 0xFFFF).astype(np.uint16), (w[:, 1] >> 16).astype(np.uint16)

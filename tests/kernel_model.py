@@ -1,0 +1,141 @@
+"""Pure-Python model of the framesum kernel's arithmetic decomposition (test infrastructure).
+
+It mirrors seqs_amd/csrc/framesum_kernel.hip step by step — end-anchored
+64-byte rows, 4 lanes x 4 dword streams per frame with A <- Z64(A) ^ w,
+the intra-lane Z4 Horner, the Z32/Z16 lane tree, the final Z4, the <=3-byte
+inverse step, the 4-byte init trick, and the native-domain (little-endian
+dword) one's-complement sum with exact corrections — so the algebra can be
+checked on CPU against zlib / the oracle before and independently of the GPU.
+Small inputs only.
+"""
+from __future__ import annotations
+
+import struct
+
+POLY = 0xEDB88320
+
+
+def _t1():
+    t = []
+    for i in range(256):
+        c = i
+        for _ in range(8):
+            c = (c >> 1) ^ POLY if c & 1 else c >> 1
+        t.append(c)
+    return t
+
+
+T1 = _t1()
+INV = [0] * 256
+for _j, _v in enumerate(T1):
+    INV[_v >> 24] = _j
+
+
+def zero_shift(r: int, nbytes: int) -> int:
+    for _ in range(nbytes):
+        r = (r >> 8) ^ T1[r & 0xFF]
+    return r
+
+
+def op_table(nbytes: int):
+    return [[zero_shift(v << (8 * b), nbytes) for v in range(256)] for b in range(4)]
+
+
+Z64, Z4, Z32, Z16 = op_table(64), op_table(4), op_table(32), op_table(16)
+
+
+def apply(tab, a: int) -> int:
+    return tab[0][a & 0xFF] ^ tab[1][(a >> 8) & 0xFF] ^ tab[2][(a >> 16) & 0xFF] ^ tab[3][a >> 24]
+
+
+def crc32_model(buf: bytes, S: int, length: int) -> int:
+    """CRC-32 of buf[S:S+length] computed the way the kernel does (dword grid of `buf`)."""
+    E = S + length
+    if length < 4:
+        c = 0xFFFFFFFF
+        for b in buf[S:E]:
+            c = T1[(c ^ b) & 0xFF] ^ (c >> 8)
+        return c ^ 0xFFFFFFFF
+    sdw = S >> 2
+    fp = (E + 3) >> 2
+    nd = fp - sdw
+    sa = S & 3
+    te = (E & 3) or 4
+    head_mask = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
+    init0 = head_mask
+    init1 = (1 << (8 * sa)) - 1
+    tail_mask = 0xFFFFFFFF if te == 4 else (1 << (8 * te)) - 1
+    padded = bytes(buf) + b"\0" * 8
+
+    def dword(rel):
+        i = 4 * (sdw + rel)
+        return struct.unpack_from("<I", padded, i)[0]
+
+    R = (nd + 15) // 16
+    A = [[0] * 4 for _ in range(4)]  # [lane][stream]
+    for r in range(R):
+        for lane in range(4):
+            rel = nd - 16 * R + 16 * r + 4 * lane
+            for j in range(4):
+                rj = rel + j
+                if rj < 0:
+                    dc = 0
+                else:
+                    d = dword(rj)
+                    mk, x = 0xFFFFFFFF, 0
+                    if rj == 0:
+                        mk &= head_mask
+                        x ^= init0
+                    if rj == 1:
+                        x ^= init1
+                    if rj == nd - 1:
+                        mk &= tail_mask
+                    dc = (d & mk) ^ x
+                A[lane][j] = apply(Z64, A[lane][j]) ^ dc
+    U = []
+    for lane in range(4):
+        u = apply(Z4, A[lane][0]) ^ A[lane][1]
+        u = apply(Z4, u) ^ A[lane][2]
+        u = apply(Z4, u) ^ A[lane][3]
+        U.append(u)
+    V = [apply(Z32, U[l]) ^ U[l ^ 2] for l in range(4)]
+    W = apply(Z16, V[0]) ^ V[1]
+    c = apply(Z4, W)
+    t = (4 - (E & 3)) & 3
+    for _ in range(t):
+        j = INV[c >> 24]
+        c = (((c ^ T1[j]) << 8) & 0xFFFFFFFF) | j
+    return c ^ 0xFFFFFFFF
+
+
+def l4_native_sum(buf: bytes, S: int, l4s: int, l4e: int) -> tuple[int, int]:
+    """Exact native-domain sum of frame bytes [l4s, l4e) (frame-relative) as the kernel splits it:
+    streamed inside-dwords + head/tail partial bytes. Returns (sum, parity of the L4 start)."""
+    sa = S & 3
+    sdw = S >> 2
+    a_s, a_e = sa + l4s, sa + l4e
+    in_lo, in_hi = (a_s + 3) >> 2, a_e >> 2
+    total = 0
+    padded = bytes(buf) + b"\0" * 8
+    if in_lo < in_hi:
+        for rel in range(in_lo, in_hi):
+            total += struct.unpack_from("<I", padded, 4 * (sdw + rel))[0]
+        for p in range(l4s, 4 * in_lo - sa):
+            total += buf[S + p] << (8 * ((sa + p) & 3))
+        if a_e & 3:
+            w = struct.unpack_from("<I", padded, 4 * (sdw + in_hi))[0]
+            total += w & ((1 << (8 * (a_e & 3))) - 1)
+    else:
+        for p in range(l4s, l4e):
+            total += buf[S + p] << (8 * ((sa + p) & 3))
+    return total, a_s & 1
+
+
+def fold_native_to_be(total: int, parity: int) -> int:
+    x = total
+    while x >> 16:
+        x = (x & 0xFFFF) + (x >> 16)
+    r = (~x) & 0xFFFF
+    if not parity:
+        r = ((r & 0xFF) << 8) | (r >> 8)
+    return r

@@ -1,0 +1,163 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle, bit-exact.
+
+Sizes: golden fixtures and seeded edge batches at oracle-friendly sizes; the
+full BASELINE configs (65,536 x 1500 B; 65,536 mixed 64/576/1500/9000) are
+checked element-wise against the C oracle too (it finishes them in ~1 s).
+"""
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from oracle import coracle  # noqa: E402
+from seqs_amd import Engine, pack_frames, split_digests, synth  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def engine():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def run_device(engine, buf, off, ln, mtu=0):
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(np.ascontiguousarray(buf)).to(dev)
+    to = torch.from_numpy(np.ascontiguousarray(off).astype(np.int64)).to(dev)
+    tl = torch.from_numpy(np.ascontiguousarray(ln).astype(np.int32)).to(dev)
+    out, st = engine.digest_device(tb, to, tl, mtu=mtu)
+    torch.cuda.synchronize()
+    crc, ipc, l4c = split_digests(out.cpu().numpy())
+    return crc, ipc, l4c, st.cpu().numpy()
+
+
+def check(engine, buf, off, ln, mtu=0, label=""):
+    crc, ipc, l4c, st = run_device(engine, buf, off, ln, mtu)
+    dig, est = coracle.digest_batch(buf, off, ln, mtu=mtu, nthreads=8)
+    bad = np.nonzero((crc != dig["crc32"]) | (ipc != dig["ip_csum"]) | (l4c != dig["l4_csum"]) | (st != est))[0]
+    if bad.size:
+        i = int(bad[0])
+        raise AssertionError(
+            f"{label}: {bad.size}/{len(ln)} mismatches; first i={i} len={int(ln[i])} off={int(off[i])} "
+            f"gpu=({crc[i]:#010x},{ipc[i]:#06x},{l4c[i]:#06x},{st[i]}) "
+            f"oracle=({int(dig['crc32'][i]):#010x},{int(dig['ip_csum'][i]):#06x},{int(dig['l4_csum'][i]):#06x},{est[i]})")
+    return crc, ipc, l4c, st
+
+
+def test_kat_frames(engine):
+    kats = json.load(open(os.path.join(GOLDEN, "kats.json")))
+    frames = [bytes.fromhex(t["hex"]) for t in kats["frames"]]
+    digs = engine.digest_batch(frames, mtu=2048)
+    for t, d, f in zip(kats["frames"], digs, frames):
+        assert (d.verdict, d.ip_csum, d.l4_csum) == (t["verdict"], t["ip_csum"], t["l4_csum"])
+        assert d.crc32 == zlib.crc32(f)
+    d = engine.digest_batch([b"123456789"])[0]
+    assert d.crc32 == kats["crc32_check"]["expected"]
+
+
+def test_golden_batch(engine):
+    g = json.load(open(os.path.join(GOLDEN, "batch.json")))
+    frames = [bytes.fromhex(e["hex"]) for e in g["frames"]]
+    for align in (4, 1):  # 1 = every possible start alignment
+        buf, off, ln = pack_frames(frames, align=align)
+        crc, ipc, l4c, st = run_device(engine, buf, off, ln)
+        for i, e in enumerate(g["frames"]):
+            assert (int(crc[i]), int(ipc[i]), int(l4c[i]), int(st[i])) == (e["crc32"], e["ip_csum"], e["l4_csum"], e["verdict"]), i
+    buf, off, ln = pack_frames(frames, align=4)
+    crc, ipc, l4c, st = run_device(engine, buf, off, ln, mtu=600)
+    for e in g["mtu600"]:
+        i = e["index"]
+        assert (int(ipc[i]), int(l4c[i]), int(st[i])) == (e["ip_csum"], e["l4_csum"], e["verdict"])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_edge_batches_unaligned(engine, seed):
+    import framegen
+
+    frames = framegen.edge_batch(seed, n_random=400)
+    for align in (1, 2, 4, 16):
+        buf, off, ln = pack_frames(frames, align=align)
+        check(engine, buf, off, ln, label=f"seed{seed}/align{align}")
+        check(engine, buf, off, ln, mtu=1514, label=f"seed{seed}/align{align}/mtu")
+
+
+def test_frames_at_buffer_start_and_tiny(engine):
+    # a frame at offset 0 of the allocation with odd starts right after it, and sub-4-byte frames
+    rng = np.random.default_rng(4)
+    buf = rng.integers(0, 256, 4096, dtype=np.uint8)
+    off = np.array([0, 1, 2, 3, 5, 6, 7, 100, 101, 0, 0, 3], dtype=np.int64)
+    ln = np.array([40, 3, 2, 1, 0, 4, 5, 1500, 64, 0, 1, 9], dtype=np.int32)
+    check(engine, buf, off, ln, label="start")
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 255, 4097])
+def test_partial_tiles(engine, n):
+    buf, off, ln = synth.uniform_batch(n, 1500, seed=n)
+    crc, ipc, l4c, st = check(engine, buf, off, ln, label=f"n={n}")
+    assert (st == 0).all()
+
+
+def test_c2_full_config(engine):
+    # BASELINE configs[1]: 65,536 x 1500-B frames, bit-exact vs the oracle
+    buf, off, ln = synth.uniform_batch(65536, 1500, seed=1)
+    crc, ipc, l4c, st = check(engine, buf, off, ln, label="C2")
+    assert (st == 0).all()
+
+
+def test_c3_mixed_config(engine):
+    # BASELINE configs[2]: 65,536 frames cycling 64/576/1500/9000, TCP/UDP 50/50
+    buf, off, ln = synth.mixed_batch(65536, seed=2)
+    crc, ipc, l4c, st = check(engine, buf, off, ln, label="C3")
+    assert (st == 0).all()
+
+
+def test_random_lengths_large(engine):
+    rng = np.random.default_rng(7)
+    n = 20000
+    ln = rng.integers(0, 9100, n).astype(np.int32)
+    gaps = rng.integers(0, 7, n)
+    off = np.zeros(n, np.int64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.int64) + gaps[:-1])
+    buf = rng.integers(0, 256, int(off[-1] + ln[-1] + 16), dtype=np.uint8)
+    # make ~half the frames well-formed TCP/UDP so the checksum path is exercised at all lengths
+    for i in range(0, n, 2):
+        L = int(ln[i])
+        p = 6 if (i // 2) % 2 == 0 else 17
+        if L >= 54:
+            f = synth.make_frames(1, L, p, rng)[0]
+            buf[off[i] : off[i] + L] = f
+    check(engine, buf, off, ln, label="random")
+
+
+def test_corruption_detected(engine):
+    buf, off, ln = synth.uniform_batch(4096, 1500, seed=9)
+    rng = np.random.default_rng(1)
+    hit = rng.choice(4096, 300, replace=False)
+    for i in hit:
+        pos = int(off[i]) + int(rng.integers(34, 1500))
+        buf[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    crc, ipc, l4c, st = check(engine, buf, off, ln, label="corrupt")
+    assert (st[hit] == 13).sum() >= 290  # a single-bit flip in the L4 range always fails the checksum
+    assert (st[np.setdiff1d(np.arange(4096), hit)] == 0).all()
+
+
+def test_host_staged_path(engine):
+    buf, off, ln = synth.mixed_batch(4096, seed=5)
+    dig, st = engine.digest_host(buf, off.astype(np.uint64), ln.astype(np.uint32))
+    edig, est = coracle.digest_batch(buf, off, ln)
+    assert np.array_equal(dig, edig) and np.array_equal(st, est)
+
+
+def test_empty_batch(engine):
+    out, st = engine.digest_host(np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32))
+    assert out.size == 0
