@@ -6,17 +6,23 @@
 namespace framesum {
 
 // CRC-32 "zero-shift" operator tables, built on the host once per context
-// (framesum_tables.cpp) and copied into LDS by every workgroup.
+// (framesum_tables.cpp) directly in the kernel's LDS layout, so every workgroup
+// fills its LDS with plain 1-KB LDS-DMA copies (global_load_lds_dwordx4).
 // Z_k[b][v] = register value after feeding k zero bytes to a reflected
 // CRC-32 register holding (v << 8b)  -- i.e. multiplication by x^(8k) mod P.
 struct FsTables {
-    uint32_t zrow[4][256];  // Z_64 : one 64-byte frame-row (4 lanes x 16 B) of stream stride
-    uint32_t z4[4][256];    // Z_4  : one dword (intra-lane Horner + final step)
-    uint32_t z32[4][256];   // Z_32 : lane-tree level 1 (lanes l, l+2)
-    uint32_t z16[4][256];   // Z_16 : lane-tree level 2 (lanes l, l+1)
-    uint32_t t1[256];       // Z_1 byte table (standard CRC-32 table)
-    uint32_t inv[64];       // 256 bytes: inv[t1[j] >> 24] = j (one-byte un-shift)
+    // Region A (64 KB): 256 entry rows x 64 dword slots. Slot 8*b + c (c = 0..7) holds
+    // Z_64[b][e] (one 64-byte frame-row of stream stride), slot 32 + 8*b + c holds
+    // Z_4[b][e]; the 8 copies make the kernel's lookups LDS-bank-conflict-free.
+    uint32_t region_a[256][64];
+    uint32_t z32[4][256];      // Z_32 : lane-tree level 1 (lanes l, l+2)
+    uint32_t z16[4][256];      // Z_16 : lane-tree level 2 (lanes l, l+1)
+    uint32_t zfin[4][4][256];  // Z_4, Z_3, Z_2, Z_1 : final step Z_(4-t) (t = bytes of dword rounding)
+    uint32_t z48[4][256];      // Z_48 : lane 0 of the flattened lane tree
+    uint32_t z12[4][256];      // Z_12 : stream 0 of the flattened intra-lane combine
+    uint32_t z8[4][256];       // Z_8  : stream 1
 };
+static_assert(sizeof(FsTables) == 65536 + 4096 * 9, "FsTables is the LDS image (100 KB)");
 
 void build_tables(FsTables* t);
 

@@ -10,18 +10,24 @@
 //   * a wave owns a TILE of 16 frames; each frame gets a 4-lane GROUP.
 //   * a frame is cut into 64-byte ROWS anchored at its (dword-rounded) END, so
 //     the head row is the partial one; lane l of the group loads dwords
-//     [4l, 4l+4) of every row with one global_load_dwordx4 (16 B/lane).
+//     [4l, 4l+4) of every row with one global_load_dwordx4 (16 B/lane), kPrefetch
+//     rows ahead. The row loop depends only on the frame descriptor (offset,
+//     length); the header parse runs inside it (once the header rows have been
+//     captured into LDS), hidden behind the rows in flight.
 //   * CRC: each lane keeps 4 independent dword STREAMS; a stream's successive
 //     dwords are 64 B apart, so its Horner step is  A <- Z64(A) ^ w  with Z64 a
 //     fixed GF(2) linear map evaluated by 4 byte-table lookups in LDS. After the
-//     last row the 16 streams of a frame are combined (intra-lane Z4 Horner,
-//     then a 2-level lane tree with Z32/Z16 over DPP quad permutes).
-//     Leading zero rows do not change a zero-init CRC, and the <=3 zero bytes
-//     the dword rounding appends are removed by an exact one-byte inverse step.
-//   * one's-complement sum: the same registers are summed as dwords into a
-//     64-bit accumulator (exact integer, so RecvEth's Sum16 fold is reproduced
-//     bit for bit, incl. the 0x0000 / 0xFFFF edge); header bytes, the
-//     pseudo-header and the excluded words are applied by the frame's lane.
+//     last row the 16 streams of a frame are combined in 3 dependent lookups
+//     (U = Z12(A0)^Z8(A1)^Z4(A2)^A3 per lane, Z_(16(3-l)) per lane l + DPP
+//     quad xor, then a final Z_(4-t) that also removes the t <= 3 zero bytes
+//     the dword rounding appended). Leading zero rows do not change a zero-init CRC; the CRC init
+//     is applied by XOR-ing the frame's first 4 bytes with 0xFF.
+//   * one's-complement sum: the same registers are summed as dwords (exact
+//     64-bit integer, so RecvEth's Sum16 fold is reproduced bit for bit incl.
+//     the 0x0000 / 0xFFFF edge) from frame dword 10 on (frame byte >= 37 > 34);
+//     the frame's lane adds/subtracts the exact native-domain contributions of
+//     the header/IP-option bytes, the Ethernet padding, the excluded words and
+//     the pseudo-header.
 //   * LDS tables: the hot Z64 (and Z4) tables are stored as 8 copies per table
 //     in a [entry][table*8+copy] layout, 256 B per entry. Lane L = c + 8h of a
 //     32-lane bank group reads table (k+h)&3 in its k-th lookup, so the 32
@@ -38,24 +44,57 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
+#ifndef FS_PREFETCH
+#define FS_PREFETCH 4
+#endif
+#ifndef FS_PRIO
+#define FS_PRIO 1  // progress-based s_setprio in the row loop (see stream_rows)
+#endif
+#ifndef FS_DIAG
+#define FS_DIAG 0  // diagnostic builds only: 2 = no CRC lookups in the row loop, 3 = no row loads after the prefetch, 4 = no table fill (wrong results)
+#endif
+
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 16;
 constexpr int kThreads = kWave * kWavesPerBlock;
 constexpr int kFramesPerTile = 16;
 constexpr int kRowDwords = 16;
-constexpr int kPrefetch = 4;
-constexpr int kHdrChunks = 7;               // 7 x 16 B staged header bytes per frame
-constexpr int kHdrBytes = kHdrChunks * 16;  // 112
+constexpr int kPrefetch = FS_PREFETCH;
+constexpr int kHdrDwords = 28;              // frame bytes [0, 112) staged for the header parse
+constexpr int kHdrSlotBytes = 16 + 4 * kHdrDwords;  // + a 16-B guard for chunks that start before the frame
+constexpr int kStashBytes = 64;             // the frame's last row (Ethernet padding source)
+constexpr int kCsumRel0 = 10;               // streamed checksum starts at frame dword 10
 
-// LDS map (bytes).
+// LDS map (bytes). [0, 88 KB) is FsTables verbatim (filled by LDS-DMA).
 constexpr uint32_t kLdsZ32 = 65536;
 constexpr uint32_t kLdsZ16 = kLdsZ32 + 4096;
-constexpr uint32_t kLdsT1 = kLdsZ16 + 4096;
-constexpr uint32_t kLdsInv = kLdsT1 + 1024;
-constexpr uint32_t kLdsHdr = kLdsInv + 256;
-constexpr uint32_t kLdsBytes = kLdsHdr + kWavesPerBlock * kFramesPerTile * kHdrBytes;
-static_assert(kLdsHdr % 16 == 0, "header slots must be 16-B aligned");
+constexpr uint32_t kLdsZfin = kLdsZ16 + 4096;  // Z4, Z3, Z2, Z1 (4 KB each)
+constexpr uint32_t kLdsZ48 = kLdsZfin + 16384;
+constexpr uint32_t kLdsZ12 = kLdsZ48 + 4096;
+constexpr uint32_t kLdsZ8 = kLdsZ12 + 4096;
+constexpr uint32_t kLdsTables = kLdsZ8 + 4096;
+constexpr uint32_t kLdsHdr = kLdsTables;
+constexpr uint32_t kLdsStash = kLdsHdr + kWavesPerBlock * kFramesPerTile * kHdrSlotBytes;
+constexpr uint32_t kLdsBytes = kLdsStash + kWavesPerBlock * kFramesPerTile * kStashBytes;
+static_assert(kLdsHdr % 16 == 0 && kLdsStash % 16 == 0, "slots must be 16-B aligned");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+static_assert(sizeof(FsTables) == kLdsTables, "FsTables is the LDS image of the tables");
+constexpr uint32_t kTableChunks = kLdsTables / 1024;  // 1-KB LDS-DMA pieces
+constexpr uint32_t kDmaPerWave = (kTableChunks + kWavesPerBlock - 1) / kWavesPerBlock;
+
+#ifdef FS_STAMPS
+// Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
+__device__ unsigned long long g_fs_stamps[8192 * 8];
+#define FS_STAMP(k)                                                                          \
+    do {                                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+        if (lane == 0 && gwave < 8192u) g_fs_stamps[gwave * 8u + (k)] = t_;                  \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+    } while (0)
+#else
+#define FS_STAMP(k) do { } while (0)
+#endif
 
 constexpr uint32_t kZ4Off = 128;  // Z4 copies sit in slots 32..63 of each region-A entry row
 
@@ -89,7 +128,7 @@ __device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const Lane
     return t0 ^ t1 ^ t2 ^ t3;
 }
 
-// Z operator from a plain [4][256] table (region B; used twice per frame).
+// Z operator from a plain [4][256] table (region B; a few uses per frame).
 __device__ __forceinline__ uint32_t zplain(const char* lds, uint32_t a, uint32_t base) {
     return lds32(lds, base + ((a & 0xffu) << 2)) ^ lds32(lds, base + 1024 + (((a >> 8) & 0xffu) << 2)) ^
            lds32(lds, base + 2048 + (((a >> 16) & 0xffu) << 2)) ^ lds32(lds, base + 3072 + ((a >> 24) << 2));
@@ -104,29 +143,48 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xffu) <<
 
 // 16 bytes of row data for one lane: dwords [rel, rel+4) relative to the frame's
 // first dword. Issued unconditionally (no divergent branch around the load, so
-// the prefetch ring keeps kPrefetch loads in flight); rows that start before
+// the prefetch ring keeps kPrefetch-1 loads in flight); rows that start before
 // the frame are clamped to `lo` (>= the buffer start) and fixed up / masked by
 // the slow path.
 __device__ __forceinline__ u32x4 load_chunk(const uint32_t* fb, int rel, int lo) {
     return *reinterpret_cast<const u32x4_a4*>(fb + max(rel, lo));
 }
 
-// Per-frame row-mask parameters, held by every lane of the frame's group.
+// Exact 64-bit one's-complement accumulator kept as {low word, carry count}: one
+// v_add_co_u32 + v_addc_co_u32 per dword, straight from the load registers.
+struct Acc {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ void acc_add(Acc& a, uint32_t x) {
+    unsigned int c;
+    a.lo = __builtin_addc(a.lo, x, 0u, &c);
+    a.hi += c;
+}
+
+// Per-frame row parameters, held by every lane of the frame's group.
 struct RowMasks {
     int nd;              // frame dwords (incl. the partial last one); 0 = nothing to stream
-    int in_lo, in_hi;    // dwords [in_lo, in_hi) lie fully inside the L4 checksum range
     int fast_lo, fast_hi;
     uint32_t head_mask, init0, init1, tail_mask;
 };
 
-__device__ __forceinline__ void process_row(const char* lds, const LaneKeys& keys, u32x4 v, int rel, bool fast,
-                                            const RowMasks& m, int lo, uint32_t (&A)[4], uint64_t& cs) {
+__device__ __forceinline__ void process_row(char* lds, const LaneKeys& keys, u32x4 v, int rel, bool fast,
+                                            const RowMasks& m, int lo, uint32_t hdr_slot, uint32_t (&A)[4], Acc& cs) {
+    if (FS_DIAG == 2) {
+        A[0] ^= v.x; A[1] ^= v.y; A[2] ^= v.z; A[3] ^= v.w;
+        acc_add(cs, v.x); acc_add(cs, v.y); acc_add(cs, v.z); acc_add(cs, v.w);
+        return;
+    }
     if (fast) {
         A[0] = zrep(lds, A[0], keys, 0) ^ v.x;
         A[1] = zrep(lds, A[1], keys, 0) ^ v.y;
         A[2] = zrep(lds, A[2], keys, 0) ^ v.z;
         A[3] = zrep(lds, A[3], keys, 0) ^ v.w;
-        cs += (uint64_t)v.x + v.y + (uint64_t)v.z + v.w;
+        acc_add(cs, v.x);
+        acc_add(cs, v.y);
+        acc_add(cs, v.z);
+        acc_add(cs, v.w);
+        if (rel > -4 && rel < kHdrDwords) *reinterpret_cast<u32x4*>(lds + hdr_slot + 16u + 4u * (uint32_t)rel) = v;
     } else {
         const int sh = max(rel, lo) - rel;  // >0 only when the load was clamped at the buffer start
         if (sh > 0 && sh < 4) {
@@ -139,124 +197,219 @@ __device__ __forceinline__ void process_row(const char* lds, const LaneKeys& key
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int rj = rel + j;
-            const uint32_t d = v[j];
-            uint32_t mk = 0xffffffffu, x = 0u;
-            if (rj == 0) { mk &= m.head_mask; x ^= m.init0; }
-            if (rj == 1) x ^= m.init1;
-            if (rj == m.nd - 1) mk &= m.tail_mask;
-            const uint32_t dc = (rj >= 0) ? ((d & mk) ^ x) : 0u;
-            const uint32_t ds = ((uint32_t)(rj - m.in_lo) < (uint32_t)(m.in_hi - m.in_lo)) ? d : 0u;
-            A[j] = zrep(lds, A[j], keys, 0) ^ dc;
-            cs += ds;
+            uint32_t d = (rj >= 0) ? v[j] : 0u;
+            uint32_t x = 0u;
+            if (rj == 0) { d &= m.head_mask; x = m.init0; }
+            if (rj == 1) x = m.init1;
+            if (rj == m.nd - 1) d &= m.tail_mask;
+            A[j] = zrep(lds, A[j], keys, 0) ^ (d ^ x);
+            acc_add(cs, (rj >= kCsumRel0) ? d : 0u);
         }
+        // the frame's first 112 bytes go to the header slot (chunks starting before the frame
+        // spill their garbage part into the slot's 16-B guard)
+        if (rel > -4 && rel < kHdrDwords) *reinterpret_cast<u32x4*>(lds + hdr_slot + 16u + 4u * (uint32_t)rel) = v;
     }
 }
 
-// Header parse of one frame from its LDS staging slot (frame byte p at slot[sa + p]).
-struct Parsed {
-    uint32_t verdict;
-    uint32_t ip_csum;
-    uint32_t stored;     // stored L4 checksum word (BE value)
-    int compute;         // 0 none, 1 L4 checksum computed
-    int use_main;        // add the streamed inside-dword sum
-    int in_lo, in_hi;
-    int parity;          // absolute parity of the L4 start (1 = odd)
-    int64_t corr;        // exact native-domain corrections
-    int tail_nb;         // bytes of the partial dword at in_hi that belong to L4 (0 = none)
-};
-
-__device__ __forceinline__ uint32_t hb(const char* lds, uint32_t slot, uint32_t p) { return lds8(lds, slot + p); }
-__device__ __forceinline__ uint32_t hbe16(const char* lds, uint32_t slot, uint32_t p) {
-    return (hb(lds, slot, p) << 8) | hb(lds, slot, p + 1);
+// ---- frame-lane helpers over the LDS header slot (absolute-dword aligned: slot
+// dword k = frame-relative dword k, frame byte p at slot byte sa + p).
+__device__ __forceinline__ uint32_t slot_dw(const char* lds, uint32_t slot, uint32_t k) { return lds32(lds, slot + 16u + 4u * k); }
+// frame bytes [4j, 4j+4) as a little-endian dword
+__device__ __forceinline__ uint32_t frame_dw(const char* lds, uint32_t slot, uint32_t sa, uint32_t j) {
+    return __builtin_amdgcn_alignbyte(slot_dw(lds, slot, j + 1), slot_dw(lds, slot, j), sa);
+}
+// bytes of absolute dword k that lie in the absolute byte range [a0, a1)
+__device__ __forceinline__ uint32_t range_mask(int k, int a0, int a1) {
+    const int lo = min(max(a0 - 4 * k, 0), 4), hi = min(max(a1 - 4 * k, 0), 4);
+    const uint32_t mhi = (hi >= 4) ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
+    const uint32_t mlo = (lo >= 4) ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
+    return mhi & ~mlo;
+}
+// exact native-domain sum (byte at absolute address a weighs 256^(a mod 4)) of
+// frame bytes [p0, p1) taken from a dword-aligned LDS image whose dword 0 is
+// frame-relative dword `d0` at byte `base` (slot: base = slot + 16, d0 = 0; stash: d0 = nd - 16).
+__device__ uint64_t nsum_lds(const char* lds, uint32_t base, int d0, int ndw, uint32_t sa, int p0, int p1) {
+    uint64_t s = 0;
+    if (p1 <= p0) return s;
+    const int a0 = (int)sa + p0, a1 = (int)sa + p1;
+    for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) {
+        const int i = k - d0;
+        if (i >= 0 && i < ndw) s += lds32(lds, base + 4u * (uint32_t)i) & range_mask(k, a0, a1);
+    }
+    return s;
 }
 
-__device__ Parsed parse_frame(const char* lds, uint32_t slot /* byte addr of frame byte 0 */, uint32_t sa,
-                              uint32_t len, uint32_t mtu) {
-    Parsed r;
-    r.verdict = V_OK;
-    r.ip_csum = 0;
-    r.stored = 0;
-    r.compute = 0;
-    r.use_main = 0;
-    r.in_lo = 0;
-    r.in_hi = 0;
-    r.parity = 0;
-    r.corr = 0;
-    r.tail_nb = 0;
-    if (len < 34) { r.verdict = V_SMOL; return r; }                       // portstack.go:167-168
-    if (mtu != 0 && len > mtu) { r.verdict = V_MTU; return r; }           // :169-172
-    {   // eth/headers.go:333-340 via Put (:289-301): version forced to 4, checksum zeroed, 20 bytes.
-        uint32_t s = (((0x40u | (hb(lds, slot, 14) & 0xfu)) << 8) | hb(lds, slot, 15));
+// Header parse result of one frame (frame lane), computed while its rows stream.
+struct Parsed {
+    uint32_t verdict;   // final unless `compute`
+    uint32_t ip_csum;
+    uint32_t stored;    // stored L4 checksum (BE)
+    int compute;        // the L4 checksum is computed
+    int parity;         // absolute parity of the L4 start (1 = odd)
+    uint32_t end;       // IP datagram end (frame-relative): Ethernet padding is [end, len)
+    int64_t corr;       // exact native-domain corrections except the padding
+};
+
+// Header parse for one frame (frame lane). Gates follow stacks/portstack.go:163-308
+// exactly (oracle/framesum_oracle.c restates them line by line; the parity tests
+// compare the two). Reads only the LDS header slot.
+__device__ Parsed parse_frame(const char* lds, uint32_t slot, uint32_t sa, uint32_t len, uint32_t mtu) {
+    Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0};
+    if (len < 34u) { r.verdict = V_SMOL; return r; }                          // portstack.go:167-168
+    if (mtu != 0 && len > mtu) { r.verdict = V_MTU; return r; }              // :169-172
+    uint32_t bs[9];                                                           // bswap32(frame dword j), j = 3..8
 #pragma unroll
-        for (uint32_t p = 16; p < 34; p += 2)
-            if (p != 24) s += hbe16(lds, slot, p);
+    for (uint32_t j = 3; j < 9; ++j) bs[j] = __builtin_bswap32(frame_dw(lds, slot, sa, j));
+    const uint32_t etype = bs[3] >> 16;                                       // headers.go:209-215
+    const uint32_t vihl = (bs[3] >> 8) & 0xffu;
+    {   // eth/headers.go:333-340 via Put (:289-301): version forced to 4, checksum zeroed, 20 bytes.
+        uint32_t s = ((0x40u | (vihl & 0xfu)) << 8) | (bs[3] & 0xffu);
+        s += (bs[4] >> 16) + (bs[4] & 0xffffu) + (bs[5] >> 16) + (bs[5] & 0xffffu) + (bs[6] & 0xffffu) +
+             (bs[7] >> 16) + (bs[7] & 0xffffu) + (bs[8] >> 16);
         s = (s & 0xffffu) + (s >> 16);
         s = (s & 0xffffu) + (s >> 16);
         r.ip_csum = (~s) & 0xffffu;
     }
-    const uint32_t etype = hbe16(lds, slot, 12);
     if (etype != 0x0800u && etype != 0x0806u) { r.verdict = V_NOT_IPV4; return r; }  // :187-188
-    if (etype == 0x0806u) { r.verdict = (len < 42) ? V_SMOL : V_ARP; return r; }     // :191-197
-    const uint32_t vihl = hb(lds, slot, 14);
-    const uint32_t ipoff = (vihl & 0xfu) * 4u;                            // uint8, <= 60
-    const uint32_t off = 14u + ipoff;                                     // :201
-    const uint32_t tl = hbe16(lds, slot, 16);
-    const uint32_t end = (14u + tl) & 0xffffu;                            // :202 uint16 wrap
-    if ((vihl >> 4) != 4u) { r.verdict = V_IPVER; return r; }             // :204
-    if (ipoff < 20u) { r.verdict = V_IHL; return r; }                     // :206
+    if (etype == 0x0806u) { r.verdict = (len < 42u) ? V_SMOL : V_ARP; return r; }     // :191-197
+    const uint32_t ipoff = (vihl & 0xfu) * 4u;                                // uint8, <= 60
+    const uint32_t off = 14u + ipoff;                                         // :201
+    const uint32_t tl = bs[4] >> 16;
+    const uint32_t end = (14u + tl) & 0xffffu;                                // :202 uint16 wrap
+    if ((vihl >> 4) != 4u) { r.verdict = V_IPVER; return r; }                 // :204
+    if (ipoff < 20u) { r.verdict = V_IHL; return r; }                         // :206
     if (off > end || off > len || end > len) { r.verdict = V_BADLEN; return r; }  // :211
-    if (mtu != 0 && end > mtu) { r.verdict = V_MTU; return r; }           // :213
+    if (mtu != 0 && end > mtu) { r.verdict = V_MTU; return r; }               // :213
     const uint32_t l4len = end - off;
-    const uint32_t proto = hb(lds, slot, 23);
-    uint32_t lenword, skip0;
-    if (proto == 17u) {                                                   // :222-244
+    const uint32_t proto = bs[5] & 0xffu;
+    // L4 header: off = 4q + 2 (q = 3 + IHL); frame dwords q .. q+5 cover bytes off-2 .. off+21.
+    const uint32_t q = (off - 2u) >> 2;
+    uint32_t lb[6];
+#pragma unroll
+    for (uint32_t i = 0; i < 6; ++i) lb[i] = __builtin_bswap32(frame_dw(lds, slot, sa, q + i));
+    const uint32_t sport = lb[0] & 0xffffu, dport = lb[1] >> 16;
+    uint32_t lenword, excl;
+    if (proto == 17u) {                                                       // :222-244
         if (l4len < 8u) { r.verdict = V_SHORT; return r; }
-        const uint32_t sport = hbe16(lds, slot, off), dport = hbe16(lds, slot, off + 2);
-        const uint32_t ulen = hbe16(lds, slot, off + 4);
+        const uint32_t ulen = lb[1] & 0xffffu;
         if (sport == 0 || dport == 0) { r.verdict = V_ZEROPORT; return r; }
         if (ulen < 8u) { r.verdict = V_UDPLEN; return r; }
-        lenword = ulen;                                                   // headers.go:386-390
-        skip0 = off + 6;
-        r.stored = hbe16(lds, slot, off + 6);
-    } else if (proto == 6u) {                                             // :283-308
+        lenword = ulen;                                                       // headers.go:386-390
+        r.stored = lb[2] >> 16;
+        excl = 6;                                                             // Checksum (2 bytes)
+    } else if (proto == 6u) {                                                 // :283-308
         if (l4len < 20u) { r.verdict = V_SHORT; return r; }
-        const uint32_t sport = hbe16(lds, slot, off), dport = hbe16(lds, slot, off + 2);
-        const uint32_t toff = (hbe16(lds, slot, off + 12) >> 12) * 4u;    // headers.go:477-485
+        const uint32_t toff = ((lb[3] >> 12) & 0xfu) * 4u;                    // headers.go:477-485
         if (sport == 0 || dport == 0) { r.verdict = V_ZEROPORT; return r; }
         if (toff < 20u || toff > l4len) { r.verdict = V_TCPOFF; return r; }
-        lenword = (tl - ipoff) & 0xffffu;                                 // headers.go:516
-        skip0 = off + 16;                                                 // Checksum + UrgentPtr (:518-526)
-        r.stored = hbe16(lds, slot, off + 16);
+        lenword = (tl - ipoff) & 0xffffu;                                     // headers.go:516
+        r.stored = lb[4] & 0xffffu;
+        excl = 16;                                                            // Checksum + UrgentPtr (:518-526)
     } else {
-        r.verdict = V_PROTO;                                              // :220-221
+        r.verdict = V_PROTO;                                                  // :220-221
         return r;
     }
     r.compute = 1;
-    // Native (little-endian dword) domain: byte at absolute address a weighs 256^(a mod 4).
-    const uint32_t a_s = sa + off, a_e = sa + end;
-    r.parity = (int)(a_s & 1u);
-    int in_lo = (int)((a_s + 3u) >> 2), in_hi = (int)(a_e >> 2);
-    int64_t corr = 0;
-    if (in_lo < in_hi) {
-        for (uint32_t p = off; sa + p < 4u * (uint32_t)in_lo; ++p) corr += (int64_t)(hb(lds, slot, p) << (8u * ((sa + p) & 3u)));
-        r.tail_nb = (int)(a_e & 3u);
-        r.use_main = 1;
-    } else {
-        for (uint32_t p = off; p < end; ++p) corr += (int64_t)(hb(lds, slot, p) << (8u * ((sa + p) & 3u)));
-        in_lo = in_hi = 0;
-    }
-    // Excluded words (UDP: Checksum; TCP: Checksum + UrgentPtr), exact contributions.
-    const uint32_t nskip = (proto == 6u) ? 4u : 2u;
-    for (uint32_t p = skip0; p < skip0 + nskip; ++p) corr -= (int64_t)(hb(lds, slot, p) << (8u * ((sa + p) & 3u)));
-    // Pseudo-header words (BE values), mapped to the native domain.
-    const uint32_t w[6] = {hbe16(lds, slot, 26), hbe16(lds, slot, 28), hbe16(lds, slot, 30), hbe16(lds, slot, 32),
-                           proto, lenword};
+    r.end = end;
+    // Native-domain total over [off, end) = streamed frame bytes >= P10 + these exact
+    // corrections (+ the padding correction applied at the end, from the stash).
+    const int P10 = 4 * kCsumRel0 - (int)sa;  // first streamed frame byte
+    int64_t t = 0;
+    if ((int)off < P10) t += (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, (int)off, P10);
+    else t -= (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, P10, (int)off);
+    t -= (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, (int)(off + excl),
+                           (int)(off + excl + (proto == 6u ? 4u : 2u)));
+    r.parity = (int)((sa + off) & 1u);
+    const uint32_t w[6] = {bs[6] & 0xffffu, bs[7] >> 16, bs[7] & 0xffffu, bs[8] >> 16, proto, lenword};
 #pragma unroll
-    for (int i = 0; i < 6; ++i) corr += (int64_t)(r.parity ? w[i] : bswap16(w[i]));
-    r.corr = corr;
-    r.in_lo = in_lo;
-    r.in_hi = in_hi;
+    for (int i = 0; i < 6; ++i) t += (int64_t)(r.parity ? w[i] : bswap16(w[i]));
+    r.corr = t;
     return r;
+}
+
+// Final L4 checksum + verdict (frame lane) once the streamed sum is known.
+__device__ uint32_t finish_l4(const char* lds, uint32_t stash, const uint32_t* fb, uint32_t sa, uint32_t len,
+                              uint32_t nd, const Parsed& P, uint64_t main_sum, uint32_t& verdict) {
+    int64_t t = (int64_t)main_sum + P.corr;
+    if (P.end < len) {  // Ethernet padding after the IP datagram
+        const int sd0 = (int)nd - 16;
+        if ((int)(sa + P.end) >= 4 * sd0) {
+            t -= (int64_t)nsum_lds(lds, stash, sd0, 16, sa, (int)P.end, (int)len);
+        } else {  // long padding (malformed frame): exact sum straight from global memory
+            const int a0 = (int)(sa + P.end), a1 = (int)(sa + len);
+            uint64_t s = 0;
+            for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s += fb[k] & range_mask(k, a0, a1);
+            t -= (int64_t)s;
+        }
+    }
+    uint64_t x = (uint64_t)t;
+    x = (x & 0xffffffffu) + (x >> 32);
+    while (x >> 16) x = (x & 0xffffu) + (x >> 16);
+    uint32_t l4 = (~(uint32_t)x) & 0xffffu;
+    if (!P.parity) l4 = bswap16(l4);
+    verdict = (l4 == P.stored) ? V_OK : V_CSUM;
+    return l4;
+}
+
+// Per-tile state of one wave.
+struct Tile {
+    // frame lane (lanes 0..15)
+    bool fvalid;
+    uint32_t fi, len, nd, sa, te;
+    uint64_t E, sdw;
+    // group lanes
+    int g_nd, R, Rp, Rsplit, rel0, rel_last, lo;
+    uint32_t g_sa, g_te;
+    const uint32_t* gfb;
+};
+
+__device__ __forceinline__ void tile_descriptors(Tile& T, uint32_t tile, uint32_t lane, uint32_t n,
+                                                 const uint64_t* __restrict__ offsets,
+                                                 const uint32_t* __restrict__ lengths, uint64_t& S) {
+    T.fi = tile * kFramesPerTile + lane;
+    T.fvalid = lane < (uint32_t)kFramesPerTile && T.fi < n;
+    S = 0;
+    T.len = 0;
+    if (T.fvalid) {
+        S = offsets[T.fi];
+        T.len = lengths[T.fi];
+    }
+}
+
+__device__ __forceinline__ void tile_geometry(Tile& T, uint64_t S, uint32_t lane, uint32_t grp, uint32_t gl,
+                                              const uint8_t* __restrict__ frames) {
+    T.E = S + T.len;
+    T.sdw = S >> 2;
+    const uint32_t ndall = (uint32_t)(((T.E + 3u) >> 2) - T.sdw);
+    T.nd = (T.fvalid && T.len >= 4u) ? ndall : 0u;
+    T.sa = (uint32_t)(S & 3u);
+    T.te = (uint32_t)(T.E & 3u) ? (uint32_t)(T.E & 3u) : 4u;
+    // group lanes (rebuilt from the kernel argument so loads stay global_load, not flat_load)
+    const uint32_t sdw_lo = (uint32_t)__shfl((int)(uint32_t)T.sdw, (int)grp);
+    const uint32_t sdw_hi = (uint32_t)__shfl((int)(uint32_t)(T.sdw >> 32), (int)grp);
+    T.gfb = reinterpret_cast<const uint32_t*>(frames + ((((uint64_t)sdw_hi << 32) | sdw_lo) << 2));
+    T.g_nd = __shfl((int)T.nd, (int)grp);
+    T.g_sa = (uint32_t)__shfl((int)T.sa, (int)grp);
+    T.g_te = (uint32_t)__shfl((int)T.te, (int)grp);
+    uint32_t rows = (lane < (uint32_t)kFramesPerTile) ? (T.nd + kRowDwords - 1) / kRowDwords : 0u;
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) rows = max(rows, (uint32_t)__shfl_xor((int)rows, m));
+    T.R = __builtin_amdgcn_readfirstlane((int)rows);
+    // Rows padded at the FRONT to a multiple of kPrefetch: leading all-zero rows
+    // leave a zero-init CRC stream unchanged, so the loop needs no tail guard.
+    T.Rp = (T.R + kPrefetch - 1) / kPrefetch * kPrefetch;
+    // Rsplit: first row (multiple of kPrefetch) by which every frame's header dwords
+    // [0, 28) have streamed through the slot; the header parse runs there.
+    int rh = -1;
+    if (lane < (uint32_t)kFramesPerTile && T.nd > 0)
+        rh = (min(kHdrDwords - 1, (int)T.nd - 1) - ((int)T.nd - kRowDwords * T.Rp)) / kRowDwords;
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) rh = max(rh, __shfl_xor(rh, m));
+    rh = __builtin_amdgcn_readfirstlane(rh);
+    T.Rsplit = min(T.Rp, (rh + kPrefetch) / kPrefetch * kPrefetch);
+    T.rel0 = T.g_nd - kRowDwords * T.Rp + 4 * (int)gl;
+    T.rel_last = T.rel0 + kRowDwords * (T.Rp - 1);
+    T.lo = (sdw_hi != 0 || sdw_lo > (1u << 24)) ? -(1 << 24) : -(int)sdw_lo;  // never below frames[0]
 }
 
 __global__ void __launch_bounds__(kThreads, 1)
@@ -265,21 +418,6 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
               uint2* __restrict__ out, uint8_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
 
-    // ---- LDS table fill: region A (replicated Z64 | Z4), region B (Z32, Z16, T1, inv).
-    for (uint32_t w = threadIdx.x; w < 4096u; w += kThreads) {
-        const uint32_t e = w >> 4, slot0 = (w & 15u) * 4u;
-        const uint32_t b = (slot0 & 31u) >> 3;
-        const uint32_t val = (slot0 < 32u) ? tabs->zrow[b][e] : tabs->z4[b][e];
-        u32x4 v4 = {val, val, val, val};
-        *reinterpret_cast<u32x4*>(lds + e * 256u + slot0 * 4u) = v4;
-    }
-    {
-        const uint32_t* src = &tabs->z32[0][0];  // z32, z16, t1, inv are contiguous
-        uint32_t* dst = reinterpret_cast<uint32_t*>(lds + kLdsZ32);
-        for (uint32_t i = threadIdx.x; i < (kLdsHdr - kLdsZ32) / 4u; i += kThreads) dst[i] = src[i];
-    }
-    __syncthreads();
-
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t grp = lane >> 2;   // frame slot of this lane's group
@@ -287,8 +425,12 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     const uint32_t gwave = blockIdx.x * kWavesPerBlock + wave;
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
     const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
-    const uint32_t hdr_base = kLdsHdr + wave * (kFramesPerTile * kHdrBytes);
+    const uint32_t hdr_base = kLdsHdr + wave * (kFramesPerTile * kHdrSlotBytes);
+    const uint32_t stash_base = kLdsStash + wave * (kFramesPerTile * kStashBytes);
 
+    const uint32_t slot = hdr_base + (lane & 15u) * kHdrSlotBytes;       // frame lane's slot
+    const uint32_t gslot = hdr_base + grp * kHdrSlotBytes;               // group's slot
+    const uint32_t stash = stash_base + (lane & 15u) * kStashBytes;      // frame lane's last-row stash
     LaneKeys keys;
     {
         const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
@@ -302,165 +444,148 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         }
     }
 
-    for (uint32_t tile = gwave; tile < ntiles; tile += nwaves) {
-        // ---- frame lanes (0..15): descriptor, header staging.
-        const uint32_t fi = tile * kFramesPerTile + lane;
-        const bool fvalid = lane < (uint32_t)kFramesPerTile && fi < n;
-        uint64_t S = 0;
-        uint32_t len = 0;
-        if (fvalid) {
-            S = offsets[fi];
-            len = lengths[fi];
-        }
-        const uint64_t E = S + len;
-        const uint64_t sdw = S >> 2;
-        const uint32_t ndall = (uint32_t)(((E + 3u) >> 2) - sdw);
-        const uint32_t nd = (fvalid && len >= 4u) ? ndall : 0u;
-        const uint32_t sa = (uint32_t)(S & 3u);
-        const uint32_t te = (uint32_t)(E & 3u) ? (uint32_t)(E & 3u) : 4u;  // valid bytes in last dword
-        const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + sdw * 4u);
-        const uint32_t slot = hdr_base + (lane & 15u) * kHdrBytes;
-        if (fvalid) {
+    // Preamble, ordered so that only ONE memory round trip precedes the first row's
+    // load: the table LDS-DMA and the first tile's descriptors are issued back to back
+    // (hipcc does not count LDS-DMA in its vmcnt model, so the descriptors go last),
+    // then the row prefetch; the tables are waited for just before the first lookup.
+    uint32_t tile = gwave;
+    FS_STAMP(0);
+    Tile T;
+    uint64_t S;
+    u32x4 pf[kPrefetch];
+    {   // exactly kDmaPerWave pieces per wave (a static count keeps the compiler's vmcnt
+        // bookkeeping exact); surplus pieces re-copy the last chunk with identical bytes
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
-            for (uint32_t k = 0; k < (uint32_t)kHdrChunks; ++k) {
-                const uint32_t d0 = 4u * k;
-                if (d0 < ndall) {
-                    u32x4 v = {0u, 0u, 0u, 0u};
-                    if (d0 + 4u <= ndall) {
-                        v = *reinterpret_cast<const u32x4_a4*>(fb + d0);
-                    } else {
-                        v.x = fb[d0];
-                        if (d0 + 1u < ndall) v.y = fb[d0 + 1];
-                        if (d0 + 2u < ndall) v.z = fb[d0 + 2];
-                    }
-                    *reinterpret_cast<u32x4*>(lds + slot + 16u * k) = v;
-                }
-            }
+        for (uint32_t k = 0; k < (FS_DIAG == 4 ? 0u : kDmaPerWave); ++k) {
+            const uint32_t c = min(w0 + k * kWavesPerBlock, kTableChunks - 1u);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
+                                             lds + c * 1024u, 16, 0, 0);
         }
-
-        // ---- group lanes: frame geometry from the frame lane, wave row count.
-        // (rebuilt from the kernel argument so the loads stay global_load, not flat_load)
-        const uint32_t sdw_lo = (uint32_t)__shfl((int)(uint32_t)sdw, (int)grp);
-        const uint32_t sdw_hi = (uint32_t)__shfl((int)(uint32_t)(sdw >> 32), (int)grp);
-        const uint32_t* gfb = reinterpret_cast<const uint32_t*>(frames + ((((uint64_t)sdw_hi << 32) | sdw_lo) << 2));
-        const int g_nd = __shfl((int)nd, (int)grp);
-        const uint32_t g_sa = (uint32_t)__shfl((int)sa, (int)grp);
-        const uint32_t g_te = (uint32_t)__shfl((int)te, (int)grp);
-
-        uint32_t rows = (lane < (uint32_t)kFramesPerTile) ? (nd + kRowDwords - 1) / kRowDwords : 0u;
+    }
+    tile_descriptors(T, tile, lane, n, offsets, lengths, S);  // after the DMA: one shared round trip
+    if (__builtin_amdgcn_readfirstlane(tile) < ntiles) {
+        tile_geometry(T, S, lane, grp, gl, frames);
 #pragma unroll
-        for (int m = 8; m >= 1; m >>= 1) rows = max(rows, (uint32_t)__shfl_xor((int)rows, m));
-        const int R = __builtin_amdgcn_readfirstlane((int)rows);
-        // Rows padded at the FRONT to a multiple of kPrefetch: leading all-zero rows
-        // leave a zero-init CRC stream unchanged, so the loop needs no tail guard.
-        const int Rp = (R + kPrefetch - 1) / kPrefetch * kPrefetch;
-        const int rel0 = g_nd - kRowDwords * Rp + 4 * (int)gl;
-        // lowest dword index a load may touch: the buffer start (frames[0])
-        const int lo = (sdw_hi != 0 || sdw_lo > (1u << 24)) ? -(1 << 24) : -(int)sdw_lo;
+        for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
+        __builtin_amdgcn_s_waitcnt(0x0f70 | kPrefetch);  // vmcnt(kPrefetch): the table pieces are older
+    } else {
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    }
+    __builtin_amdgcn_s_barrier();  // LDS tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    FS_STAMP(1);
 
-        u32x4 pf[kPrefetch];
-#pragma unroll
-        for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(gfb, rel0 + kRowDwords * i, lo);
-
-        // ---- frame lanes: header parse (LDS slot), tail partial dword of the L4 range.
-        Parsed P;
-        uint32_t tail_word = 0;
-        if (fvalid) {
-            P = parse_frame(lds, slot + sa, sa, len, mtu);
-            if (P.compute && P.tail_nb) tail_word = fb[P.in_hi] & ((1u << (8u * (uint32_t)P.tail_nb)) - 1u);
-        } else {
-            P.verdict = V_OK; P.ip_csum = 0; P.stored = 0; P.compute = 0; P.use_main = 0;
-            P.in_lo = 0; P.in_hi = 0; P.parity = 0; P.corr = 0; P.tail_nb = 0;
-        }
-        const int use_lo = P.use_main ? P.in_lo : 0;
-        const int use_hi = P.use_main ? P.in_hi : (int)nd;
-
+    while (tile < ntiles) {
         RowMasks M;
-        M.nd = g_nd;
-        M.in_lo = __shfl(use_lo, (int)grp);
-        M.in_hi = __shfl(use_hi, (int)grp);
-        if (g_nd > 0) {
-            M.fast_lo = max(2, M.in_lo);
-            M.fast_hi = min(g_nd - 5, M.in_hi - 4);
+        M.nd = T.g_nd;
+        if (T.g_nd > 0) {
+            M.fast_lo = kCsumRel0;
+            M.fast_hi = T.g_nd - 5;
         } else {  // empty group: every row streams zeros
             M.fast_lo = -0x40000000;
             M.fast_hi = 0x40000000;
         }
-        M.head_mask = 0xffffffffu << (8u * g_sa);
+        M.head_mask = 0xffffffffu << (8u * T.g_sa);
         M.init0 = M.head_mask;
-        M.init1 = (1u << (8u * g_sa)) - 1u;
-        M.tail_mask = (g_te == 4u) ? 0xffffffffu : ((1u << (8u * g_te)) - 1u);
+        M.init1 = (1u << (8u * T.g_sa)) - 1u;
+        M.tail_mask = (T.g_te == 4u) ? 0xffffffffu : ((1u << (8u * T.g_te)) - 1u);
 
-        // ---- main loop: rows 0..Rp-1, kPrefetch rows in flight.
+        // ---- main loop: rows 0..Rp-1, kPrefetch rows in flight, split at Rsplit for the header parse.
         uint32_t A[4] = {0u, 0u, 0u, 0u};
-        uint64_t cs = 0;
-        const int rel_last = rel0 + kRowDwords * (Rp - 1);
-        for (int r0 = 0; r0 < Rp; r0 += kPrefetch) {
+        Acc acc = {0u, 0u};
+        auto stream_rows = [&](int rbeg, int rend) {
+            for (int r0 = rbeg; r0 < rend; r0 += kPrefetch) {
+                // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
+                // so without this the youngest of a SIMD's 4 waves finishes last and sets
+                // the kernel time. A wave with more rows left gets a higher priority.
+                if (FS_PRIO) {
+                    const int left4 = (4 * (T.Rp - r0)) / max(T.Rp, 1);  // 4 .. 1
+                    if (left4 >= 4) __builtin_amdgcn_s_setprio(3);
+                    else if (left4 == 3) __builtin_amdgcn_s_setprio(2);
+                    else if (left4 == 2) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
 #pragma unroll
-            for (int i = 0; i < kPrefetch; ++i) {
-                const int rel = rel0 + kRowDwords * (r0 + i);
-                const u32x4 v = pf[i];
-                pf[i] = load_chunk(gfb, min(rel + kRowDwords * kPrefetch, rel_last), lo);
-                const bool lane_fast = rel >= M.fast_lo && rel <= M.fast_hi;
-                const bool fast = __all(lane_fast);
-                process_row(lds, keys, v, rel, fast, M, lo, A, cs);
+                for (int i = 0; i < kPrefetch; ++i) {
+                    const int rel = T.rel0 + kRowDwords * (r0 + i);
+                    const bool lane_fast = rel >= M.fast_lo && rel <= M.fast_hi;
+                    const bool fast = __all(lane_fast);
+                    // consume the ring slot, then refill the SAME registers: no copy of an
+                    // in-flight load, so the compiler keeps kPrefetch-1 loads outstanding
+                    process_row(lds, keys, pf[i], rel, fast, M, T.lo, gslot, A, acc);
+                    if (FS_DIAG != 3) pf[i] = load_chunk(T.gfb, min(rel + kRowDwords * kPrefetch, T.rel_last), T.lo);
+                }
             }
-        }
+        };
+        stream_rows(0, T.Rsplit);
+        // header parse while the next kPrefetch rows are in flight
+        Parsed P = {V_OK, 0u, 0u, 0, 0, 0u, 0};
+        if (T.fvalid) P = parse_frame(lds, slot, T.sa, T.len, mtu);
+        stream_rows(T.Rsplit, T.Rp);
+        FS_STAMP(2);
+        // the refills of the last rows all re-read the final row: stash it for the padding sum
+        *reinterpret_cast<u32x4*>(lds + stash_base + grp * kStashBytes + 16u * gl) = pf[0];
 
-        // ---- combine the 16 streams of each frame (see header comment).
-        uint32_t U = zrep(lds, A[0], keys, kZ4Off) ^ A[1];
-        U = zrep(lds, U, keys, kZ4Off) ^ A[2];
-        U = zrep(lds, U, keys, kZ4Off) ^ A[3];
-        uint32_t V = zplain(lds, U, kLdsZ32) ^ dpp_quad<kQuadXor2>(U);
-        uint32_t W = zplain(lds, V, kLdsZ16) ^ dpp_quad<kQuadXor1>(V);
-        const uint32_t C = zrep(lds, W, keys, kZ4Off);
-        uint32_t cs_lo = (uint32_t)cs, cs_hi = (uint32_t)(cs >> 32);
+        // ---- combine the 16 streams of each frame: C = Z_(4-t)( xor_l Z_16(3-l)( U_l ) ),
+        //      U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3   (3 dependent LDS round trips).
+        const uint32_t U = zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zrep(lds, A[2], keys, kZ4Off) ^ A[3];
+        const uint32_t ybase = (gl == 0u) ? kLdsZ48 : (gl == 1u) ? kLdsZ32 : kLdsZ16;
+        uint32_t Y = zplain(lds, U, ybase);
+        if (gl == 3u) Y = U;
+        Y ^= dpp_quad<kQuadXor1>(Y);
+        Y ^= dpp_quad<kQuadXor2>(Y);
+        const uint32_t tpad = (4u - T.g_te) & 3u;  // zero bytes appended by the dword rounding
+        const uint32_t C = zplain(lds, Y, kLdsZfin + 4096u * tpad);
+        uint64_t cs = ((uint64_t)acc.hi << 32) | acc.lo;
         {   // 64-bit sum over the 4 lanes of the group
-            uint64_t t = ((uint64_t)dpp_quad<kQuadXor1>(cs_hi) << 32) | dpp_quad<kQuadXor1>(cs_lo);
+            uint64_t t = ((uint64_t)dpp_quad<kQuadXor1>(acc.hi) << 32) | dpp_quad<kQuadXor1>(acc.lo);
             cs += t;
-            cs_lo = (uint32_t)cs;
-            cs_hi = (uint32_t)(cs >> 32);
-            t = ((uint64_t)dpp_quad<kQuadXor2>(cs_hi) << 32) | dpp_quad<kQuadXor2>(cs_lo);
+            t = ((uint64_t)dpp_quad<kQuadXor2>((uint32_t)(cs >> 32)) << 32) | dpp_quad<kQuadXor2>((uint32_t)cs);
             cs += t;
         }
         const uint32_t src = (lane & 15u) * 4u;
         uint32_t crcv = (uint32_t)__shfl((int)C, (int)src);
-        const uint64_t csum =
-            ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cs >> 32), (int)src) << 32) |
-            (uint32_t)__shfl((int)(uint32_t)cs, (int)src);
+        const uint64_t csum = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cs >> 32), (int)src) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)cs, (int)src);
 
-        // ---- frame lanes: finalize + store.
-        if (fvalid) {
-            if (len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
+        FS_STAMP(3);
+        // ---- frame lanes: finish and store.
+        if (T.fvalid) {
+            if (T.len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
                 uint32_t c = 0xffffffffu;
-                for (uint32_t p = 0; p < len; ++p)
-                    c = lds32(lds, kLdsT1 + (((c ^ lds8(lds, slot + sa + p)) & 0xffu) << 2)) ^ (c >> 8);
+                const uint8_t* fbytes = frames + T.E - T.len;
+                for (uint32_t p = 0; p < T.len; ++p)
+                    c = lds32(lds, kLdsZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
                 crcv = ~c;
             } else {
-                uint32_t c = crcv;
-                const uint32_t t = (4u - (uint32_t)(E & 3u)) & 3u;  // zero bytes appended by dword rounding
-                for (uint32_t k = 0; k < t; ++k) {
-                    const uint32_t j = lds8(lds, kLdsInv + (c >> 24));
-                    c = ((c ^ lds32(lds, kLdsT1 + (j << 2))) << 8) | j;
-                }
-                crcv = ~c;
+                crcv = ~crcv;
             }
-            uint32_t verdict = P.verdict, l4 = 0;
+            uint32_t verdict = P.verdict, l4 = 0u;
             if (P.compute) {
-                uint64_t x = (uint64_t)((int64_t)(P.use_main ? csum : 0u) + P.corr) + tail_word;
-                x = (x & 0xffffffffu) + (x >> 32);
-                while (x >> 16) x = (x & 0xffffu) + (x >> 16);
-                l4 = (~(uint32_t)x) & 0xffffu;
-                if (!P.parity) l4 = bswap16(l4);
-                verdict = (l4 == P.stored) ? V_OK : V_CSUM;
+                const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + T.sdw * 4u);
+                l4 = finish_l4(lds, stash, fb, T.sa, T.len, T.nd, P, csum, verdict);
             }
-            out[fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
-            if (status) status[fi] = (uint8_t)verdict;
+            out[T.fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
+            if (status) status[T.fi] = (uint8_t)verdict;
+        }
+        FS_STAMP(4);
+        tile += nwaves;
+        if (tile < ntiles) {  // next tile: descriptors, geometry, row prefetch
+            tile_descriptors(T, tile, lane, n, offsets, lengths, S);
+            tile_geometry(T, S, lane, grp, gl, frames);
+#pragma unroll
+            for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
         }
     }
 }
 
 }  // namespace
+
+#ifdef FS_STAMPS
+extern "C" int fs_debug_read_stamps(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fs_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,

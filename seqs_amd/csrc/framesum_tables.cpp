@@ -36,21 +36,26 @@ void op_table(const uint32_t t1[256], int nbytes, uint32_t out[4][256]) {
 
 void build_tables(FsTables* t) {
     std::memset(t, 0, sizeof(*t));
-    byte_table(t->t1);
-    op_table(t->t1, 64, t->zrow);
-    op_table(t->t1, 4, t->z4);
-    op_table(t->t1, 32, t->z32);
-    op_table(t->t1, 16, t->z16);
-    // One-byte inverse: the top byte of t1[j] identifies j (it is a permutation).
-    uint8_t inv[256];
-    bool seen[256] = {false};
-    for (uint32_t j = 0; j < 256; ++j) {
-        const uint32_t top = t->t1[j] >> 24;
-        if (seen[top]) throw std::logic_error("CRC-32 table top bytes are not a permutation");
-        seen[top] = true;
-        inv[top] = (uint8_t)j;
-    }
-    std::memcpy(t->inv, inv, sizeof(inv));
+    uint32_t t1[256];
+    byte_table(t1);
+    static uint32_t zrow[4][256], z4[4][256];
+    op_table(t1, 64, zrow);
+    op_table(t1, 4, z4);
+    for (uint32_t e = 0; e < 256; ++e)
+        for (uint32_t b = 0; b < 4; ++b)
+            for (uint32_t c = 0; c < 8; ++c) {
+                t->region_a[e][8 * b + c] = zrow[b][e];
+                t->region_a[e][32 + 8 * b + c] = z4[b][e];
+            }
+    op_table(t1, 32, t->z32);
+    op_table(t1, 16, t->z16);
+    for (int k = 0; k < 4; ++k) op_table(t1, 4 - k, t->zfin[k]);
+    op_table(t1, 48, t->z48);
+    op_table(t1, 12, t->z12);
+    op_table(t1, 8, t->z8);
+    // The final step Z_(4-t) replaces "Z_4 then undo t appended zero bytes"; Z_1[0] is the
+    // standard byte table used for frames shorter than 4 bytes.
+    if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");
 }
 
 }  // namespace framesum

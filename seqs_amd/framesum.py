@@ -20,7 +20,8 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libframesum.so")
+_LIB_PATH = os.environ.get("FRAMESUM_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "lib", "libframesum.so")
 
 FS_SUCCESS = 0
 FS_E_INVALID = -1

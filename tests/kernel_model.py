@@ -2,9 +2,10 @@
 
 It mirrors seqs_amd/csrc/framesum_kernel.hip step by step — end-anchored
 64-byte rows, 4 lanes x 4 dword streams per frame with A <- Z64(A) ^ w,
-the intra-lane Z4 Horner, the Z32/Z16 lane tree, the final Z4, the <=3-byte
-inverse step, the 4-byte init trick, and the native-domain (little-endian
-dword) one's-complement sum with exact corrections — so the algebra can be
+the intra-lane Z4 Horner, the Z32/Z16 lane tree, the final Z_(4-t) step that
+also removes the <=3 zero bytes of the dword rounding, the 4-byte init trick,
+and the native-domain (little-endian dword) one's-complement sum streamed from
+frame dword 10 with exact head/padding corrections — so the algebra can be
 checked on CPU against zlib / the oracle before and independently of the GPU.
 Small inputs only.
 """
@@ -42,6 +43,7 @@ def op_table(nbytes: int):
 
 
 Z64, Z4, Z32, Z16 = op_table(64), op_table(4), op_table(32), op_table(16)
+ZFIN = [op_table(4 - t) for t in range(4)]  # final step Z_(4-t)
 
 
 def apply(tab, a: int) -> int:
@@ -100,35 +102,41 @@ def crc32_model(buf: bytes, S: int, length: int) -> int:
         U.append(u)
     V = [apply(Z32, U[l]) ^ U[l ^ 2] for l in range(4)]
     W = apply(Z16, V[0]) ^ V[1]
-    c = apply(Z4, W)
-    t = (4 - (E & 3)) & 3
-    for _ in range(t):
-        j = INV[c >> 24]
-        c = (((c ^ T1[j]) << 8) & 0xFFFFFFFF) | j
+    t = (4 - (E & 3)) & 3  # zero bytes appended by the dword rounding, removed by Z_(4-t)
+    c = apply(ZFIN[t], W)
     return c ^ 0xFFFFFFFF
 
 
-def l4_native_sum(buf: bytes, S: int, l4s: int, l4e: int) -> tuple[int, int]:
-    """Exact native-domain sum of frame bytes [l4s, l4e) (frame-relative) as the kernel splits it:
-    streamed inside-dwords + head/tail partial bytes. Returns (sum, parity of the L4 start)."""
+CSUM_REL0 = 10  # the kernel streams the checksum from frame dword 10
+
+
+def native_sum(buf: bytes, S: int, p0: int, p1: int) -> int:
+    """Exact native-domain sum of frame bytes [p0, p1): byte at absolute address a weighs 256^(a mod 4)."""
+    return sum(buf[S + p] << (8 * ((S + p) & 3)) for p in range(p0, p1))
+
+
+def l4_native_sum(buf: bytes, S: int, length: int, l4s: int, l4e: int) -> tuple[int, int]:
+    """The kernel's split of the L4 sum: streamed dwords rel >= 10 (tail-masked at the frame end)
+    plus the head correction [l4s, P10) or minus [P10, l4s), minus the Ethernet padding [l4e, len).
+    Returns (native sum over [l4s, l4e), parity of the absolute L4 start)."""
     sa = S & 3
     sdw = S >> 2
-    a_s, a_e = sa + l4s, sa + l4e
-    in_lo, in_hi = (a_s + 3) >> 2, a_e >> 2
-    total = 0
+    E = S + length
+    nd = ((E + 3) >> 2) - sdw
     padded = bytes(buf) + b"\0" * 8
-    if in_lo < in_hi:
-        for rel in range(in_lo, in_hi):
-            total += struct.unpack_from("<I", padded, 4 * (sdw + rel))[0]
-        for p in range(l4s, 4 * in_lo - sa):
-            total += buf[S + p] << (8 * ((sa + p) & 3))
-        if a_e & 3:
-            w = struct.unpack_from("<I", padded, 4 * (sdw + in_hi))[0]
-            total += w & ((1 << (8 * (a_e & 3))) - 1)
+    total = 0
+    for rel in range(CSUM_REL0, nd):
+        w = struct.unpack_from("<I", padded, 4 * (sdw + rel))[0]
+        if rel == nd - 1 and (E & 3):
+            w &= (1 << (8 * (E & 3))) - 1
+        total += w
+    p10 = 4 * CSUM_REL0 - sa
+    if l4s < p10:
+        total += native_sum(buf, S, l4s, p10)
     else:
-        for p in range(l4s, l4e):
-            total += buf[S + p] << (8 * ((sa + p) & 3))
-    return total, a_s & 1
+        total -= native_sum(buf, S, p10, l4s)
+    total -= native_sum(buf, S, l4e, length)
+    return total, (sa + l4s) & 1
 
 
 def fold_native_to_be(total: int, parity: int) -> int:

@@ -18,6 +18,16 @@ def test_crc_decomposition_vs_zlib():
         assert km.crc32_model(buf, pre, L) == zlib.crc32(buf[pre : pre + L])
 
 
+def test_final_step_equals_unshift():
+    rnd = random.Random(4)
+    for _ in range(200):
+        w = rnd.getrandbits(32)
+        for t in range(4):
+            c = km.apply(km.ZFIN[t], w)
+            # Z_(4-t)(W) shifted forward by t bytes is Z_4(W)
+            assert km.zero_shift(c, t) == km.apply(km.Z4, w)
+
+
 def test_tables_properties():
     # Z_a o Z_b = Z_(a+b) on random registers; the one-byte inverse undoes Z_1.
     rnd = random.Random(2)
@@ -49,7 +59,8 @@ def test_l4_native_split_matches_reference():
         buf = bytes(rnd.randbytes(pre)) + f + bytes(8)
         ihl = f[14] & 0xF
         l4s, l4e = 14 + 4 * ihl, 14 + struct.unpack(">H", f[16:18])[0]
-        total, parity = km.l4_native_sum(buf, pre, l4s, l4e)
+        total, parity = km.l4_native_sum(buf, pre, len(f), l4s, l4e)
+        assert total == km.native_sum(buf, pre, l4s, l4e)
         sa = pre & 3
         proto = f[23]
         skip0 = l4s + (16 if proto == 6 else 6)

@@ -1,0 +1,116 @@
+// HBM read-bandwidth microbenchmark for the framesum access pattern (measurement tool).
+//  k_stream : grid-stride global_load_dwordx4, 16 B/lane, fully coalesced (chip ceiling)
+//  k_frames : the digest kernel's pattern without compute — 16 frames per wave,
+//             4 lanes per frame, 64-B end-anchored rows, kPF rows in flight
+// Both rotate NB distinct 98.3 MB buffers (> 256 MiB Infinity Cache).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+__global__ void k_stream(const u32x4* __restrict__ p, size_t n16, uint32_t* out) {
+    uint32_t acc = 0;
+    size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        u32x4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    for (; i < n16; i += stride) { u32x4 a = p[i]; acc ^= a.x ^ a.y ^ a.z ^ a.w; }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// G lanes per frame (64/G frames per wave), rows of G*16 bytes anchored at the frame end.
+template <int kPF, int G>
+__global__ void __launch_bounds__(1024) k_frames(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
+                                                 uint32_t* out) {
+    constexpr int FPW = 64 / G, RD = 4 * G;  // frames per wave, row dwords
+    const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
+    const uint32_t gwave = blockIdx.x * 16 + (threadIdx.x >> 6), nwaves = gridDim.x * 16;
+    const uint32_t ntiles = (nframes + FPW - 1) / FPW;
+    uint32_t acc = 0;
+    for (uint32_t t = gwave; t < ntiles; t += nwaves) {
+        uint32_t f = t * FPW + grp;
+        if (f >= nframes) f = nframes - 1;
+        const uint64_t S = (uint64_t)f * flen, E = S + flen;
+        const uint64_t sdw = S >> 2;
+        const int nd = (int)(((E + 3) >> 2) - sdw);
+        const int R = (nd + RD - 1) / RD;
+        const int Rp = (R + kPF - 1) / kPF * kPF;
+        const int rel0 = nd - RD * Rp + 4 * (int)gl;
+        const int rel_last = rel0 + RD * (Rp - 1);
+        const uint32_t* fb = reinterpret_cast<const uint32_t*>(base + sdw * 4);
+        const int lo = -(int)min(sdw, (uint64_t)(1 << 24));
+        u32x4 pf[kPF];
+#pragma unroll
+        for (int i = 0; i < kPF; ++i) pf[i] = *reinterpret_cast<const u32x4_a4*>(fb + max(rel0 + RD * i, lo));
+        for (int r0 = 0; r0 < Rp; r0 += kPF) {
+#pragma unroll
+            for (int i = 0; i < kPF; ++i) {
+                const int rel = rel0 + RD * (r0 + i);
+                acc = (acc * 3) ^ pf[i].x ^ pf[i].y ^ pf[i].z ^ pf[i].w;
+                pf[i] = *reinterpret_cast<const u32x4_a4*>(fb + max(min(rel + RD * kPF, rel_last), lo));
+            }
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+int main(int argc, char** argv) {
+    const size_t nbytes = 98304000;
+    const int NB = 4, iters = 100;
+    std::vector<uint8_t*> bufs(NB);
+    for (auto& b : bufs) {
+        CHECK(hipMalloc(&b, nbytes + 4096));
+        CHECK(hipMemset(b, 0x5a, nbytes + 4096));
+    }
+    uint32_t* out;
+    CHECK(hipMalloc(&out, 64));
+    hipDeviceProp_t prop;
+    CHECK(hipGetDeviceProperties(&prop, 0));
+    int cus = prop.multiProcessorCount;
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    auto timeit = [&](auto launch, const char* name) {
+        for (int i = 0; i < 10; ++i) launch(i);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipEventRecord(a));
+        for (int i = 0; i < iters; ++i) launch(i);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        double us = ms * 1e3 / iters;
+        printf("%-44s %9.2f us/launch  %8.1f GB/s\n", name, us, nbytes / (us * 1e-6) / 1e9);
+    };
+    for (int mult : {1, 2, 4, 8}) {
+        char nm[128];
+        snprintf(nm, sizeof nm, "stream dwordx4 grid=%dx%d", cus * mult, 256);
+        timeit([&](int i) { hipLaunchKernelGGL(k_stream, dim3(cus * mult), dim3(256), 0, 0,
+                                               (const u32x4*)bufs[i % NB], nbytes / 16, out); }, nm);
+    }
+    for (int mult : {4, 8}) {
+        char nm[128];
+        snprintf(nm, sizeof nm, "stream dwordx4 +4B misaligned grid=%dx256", cus * mult);
+        timeit([&](int i) { hipLaunchKernelGGL(k_stream, dim3(cus * mult), dim3(256), 0, 0,
+                                               (const u32x4*)(bufs[i % NB] + 4), nbytes / 16 - 1, out); }, nm);
+    }
+    const uint32_t nf = 65536, fl = 1500;
+#define FR(PF, G, GRID, NAME) timeit([&](int i) { hipLaunchKernelGGL((k_frames<PF, G>), dim3(GRID), dim3(1024), 0, 0, bufs[i % NB], nf, fl, out); }, NAME)
+    FR(4, 4, cus, "frames G=4  PF=4 (current kernel pattern)");
+    FR(2, 4, cus, "frames G=4  PF=2");
+    FR(6, 4, cus, "frames G=4  PF=6");
+    FR(4, 16, cus, "frames G=16 PF=4");
+    FR(2, 16, cus, "frames G=16 PF=2");
+    FR(2, 64, cus, "frames G=64 PF=2");
+    FR(1, 64, cus, "frames G=64 PF=1");
+    FR(4, 4, cus / 2, "frames G=4  PF=4 half grid (8 waves/CU eq)");
+    FR(8, 4, cus / 2, "frames G=4  PF=8 half grid");
+    return 0;
+}
