@@ -115,7 +115,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from seqs_amd import Engine
+    from seqs_amd import Engine, shard
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -138,9 +138,6 @@ def main():
     outs = [torch.empty((n, 2), dtype=torch.int32, device=dev) for _ in range(2)]
     stats = [torch.empty((n,), dtype=torch.uint8, device=dev) for _ in range(2)]
     gather = world > 1 and not args.no_gather
-    if gather:
-        g_out = [[torch.empty((n, 2), dtype=torch.int32, device=dev) for _ in range(world)] for _ in range(2)]
-        g_st = [[torch.empty((n,), dtype=torch.uint8, device=dev) for _ in range(world)] for _ in range(2)]
     stream = torch.cuda.current_stream(dev)
 
     pending = []
@@ -154,18 +151,16 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if gather:
-            # wait for the gather that used this output slot two steps ago, then gather this step's
+            # digests of step i go to rank 0 over RCCL while step i+1's kernel runs; the
+            # output slot is reused two steps later, so wait for that slot's gather first
             while len(pending) >= 2:
-                for w in pending.pop(0):
-                    w.wait()
-            hs = [dist.gather(outs[k], g_out[k] if rank == 0 else None, dst=0, async_op=True),
-                  dist.gather(stats[k], g_st[k] if rank == 0 else None, dst=0, async_op=True)]
-            pending.append(hs)
+                pending.pop(0)()
+            _, finish = shard.gather_digests(outs[k], stats[k], world, rank, n * world, async_op=True)
+            pending.append(finish)
 
     def drain():
         while pending:
-            for w in pending.pop(0):
-                w.wait()
+            pending.pop(0)()
 
     for i in range(args.warmup):
         step(i)

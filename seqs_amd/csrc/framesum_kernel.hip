@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "framesum_internal.h"
 
 namespace framesum {
@@ -119,13 +121,20 @@ struct LaneKeys {
     uint32_t sel[4];   // v_perm selectors of the 4 lookups
 };
 
-// Z operator from replicated region A (off = 0: Z64, off = 128: Z4). Conflict-free.
-__device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const LaneKeys& k, uint32_t off) {
+// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96; gfx950 has no v_xor3).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// Z(a) ^ w with Z from replicated region A (off = 0: Z64, off = 128: Z4). Conflict-free.
+__device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const LaneKeys& k, uint32_t off, uint32_t w = 0u) {
     uint32_t t0 = lds32(lds, off + __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
     uint32_t t1 = lds32(lds, off + __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
     uint32_t t2 = lds32(lds, off + __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
     uint32_t t3 = lds32(lds, off + __builtin_amdgcn_perm(a, k.cvec, k.sel[3]));
-    return t0 ^ t1 ^ t2 ^ t3;
+    return xor3(xor3(t0, t1, t2), t3, w);
 }
 
 // Z operator from a plain [4][256] table (region B; a few uses per frame).
@@ -145,21 +154,16 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xffu) <<
 // first dword. Issued unconditionally (no divergent branch around the load, so
 // the prefetch ring keeps kPrefetch-1 loads in flight); rows that start before
 // the frame are clamped to `lo` (>= the buffer start) and fixed up / masked by
-// the slow path.
+// the slow path. Rows never run past the frame's last dword (see the segments).
 __device__ __forceinline__ u32x4 load_chunk(const uint32_t* fb, int rel, int lo) {
     return *reinterpret_cast<const u32x4_a4*>(fb + max(rel, lo));
 }
 
-// Exact 64-bit one's-complement accumulator kept as {low word, carry count}: one
-// v_add_co_u32 + v_addc_co_u32 per dword, straight from the load registers.
-struct Acc {
-    uint32_t lo, hi;
-};
-__device__ __forceinline__ void acc_add(Acc& a, uint32_t x) {
-    unsigned int c;
-    a.lo = __builtin_addc(a.lo, x, 0u, &c);
-    a.hi += c;
-}
+// One's-complement accumulation: v_sad_u16(x, 0, acc) = acc + x[15:0] + x[31:16] in ONE op.
+// x[15:0] + x[31:16] is congruent to the dword's native little-endian value mod 65535 and
+// is 0 iff the dword is 0, which is all Sum16's fold needs. A lane adds at
+// most 4096 dwords of a 64-KiB frame (< 2^30), so the 32-bit accumulator cannot wrap.
+__device__ __forceinline__ uint32_t sad16(uint32_t x, uint32_t acc) { return __builtin_amdgcn_sad_u16(x, 0u, acc); }
 
 // Per-frame row parameters, held by every lane of the frame's group.
 struct RowMasks {
@@ -169,22 +173,21 @@ struct RowMasks {
 };
 
 __device__ __forceinline__ void process_row(char* lds, const LaneKeys& keys, u32x4 v, int rel, bool fast,
-                                            const RowMasks& m, int lo, uint32_t hdr_slot, uint32_t (&A)[4], Acc& cs) {
+                                            const RowMasks& m, int lo, uint32_t (&A)[4], uint32_t& cs) {
     if (FS_DIAG == 2) {
         A[0] ^= v.x; A[1] ^= v.y; A[2] ^= v.z; A[3] ^= v.w;
-        acc_add(cs, v.x); acc_add(cs, v.y); acc_add(cs, v.z); acc_add(cs, v.w);
+        cs = sad16(v.x, cs); cs = sad16(v.y, cs); cs = sad16(v.z, cs); cs = sad16(v.w, cs);
         return;
     }
     if (fast) {
-        A[0] = zrep(lds, A[0], keys, 0) ^ v.x;
-        A[1] = zrep(lds, A[1], keys, 0) ^ v.y;
-        A[2] = zrep(lds, A[2], keys, 0) ^ v.z;
-        A[3] = zrep(lds, A[3], keys, 0) ^ v.w;
-        acc_add(cs, v.x);
-        acc_add(cs, v.y);
-        acc_add(cs, v.z);
-        acc_add(cs, v.w);
-        if (rel > -4 && rel < kHdrDwords) *reinterpret_cast<u32x4*>(lds + hdr_slot + 16u + 4u * (uint32_t)rel) = v;
+        A[0] = zrep(lds, A[0], keys, 0, v.x);
+        A[1] = zrep(lds, A[1], keys, 0, v.y);
+        A[2] = zrep(lds, A[2], keys, 0, v.z);
+        A[3] = zrep(lds, A[3], keys, 0, v.w);
+        cs = sad16(v.x, cs);
+        cs = sad16(v.y, cs);
+        cs = sad16(v.z, cs);
+        cs = sad16(v.w, cs);
     } else {
         const int sh = max(rel, lo) - rel;  // >0 only when the load was clamped at the buffer start
         if (sh > 0 && sh < 4) {
@@ -202,12 +205,25 @@ __device__ __forceinline__ void process_row(char* lds, const LaneKeys& keys, u32
             if (rj == 0) { d &= m.head_mask; x = m.init0; }
             if (rj == 1) x = m.init1;
             if (rj == m.nd - 1) d &= m.tail_mask;
-            A[j] = zrep(lds, A[j], keys, 0) ^ (d ^ x);
-            acc_add(cs, (rj >= kCsumRel0) ? d : 0u);
+            A[j] = zrep(lds, A[j], keys, 0, d ^ x);
+            cs = sad16((rj >= kCsumRel0) ? d : 0u, cs);
         }
-        // the frame's first 112 bytes go to the header slot (chunks starting before the frame
-        // spill their garbage part into the slot's 16-B guard)
-        if (rel > -4 && rel < kHdrDwords) *reinterpret_cast<u32x4*>(lds + hdr_slot + 16u + 4u * (uint32_t)rel) = v;
+    }
+}
+
+// The frame's first 112 bytes go to the group's header slot (chunks starting before the
+// frame spill their garbage part into the slot's 16-B guard). Only the leading rows call it.
+__device__ __forceinline__ void capture_header(char* lds, uint32_t hdr_slot, int rel, int lo, u32x4 v) {
+    if (rel > -4 && rel < kHdrDwords) {
+        const int sh = max(rel, lo) - rel;
+        if (sh > 0 && sh < 4) {  // clamped load at the buffer start: realign as process_row does
+            const u32x4 u = v;
+            v.w = (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
+            v.z = (sh == 1) ? u.y : (sh == 2) ? u.x : 0u;
+            v.y = (sh == 1) ? u.x : 0u;
+            v.x = 0u;
+        }
+        *reinterpret_cast<u32x4*>(lds + hdr_slot + 16u + 4u * (uint32_t)rel) = v;
     }
 }
 
@@ -225,16 +241,16 @@ __device__ __forceinline__ uint32_t range_mask(int k, int a0, int a1) {
     const uint32_t mlo = (lo >= 4) ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
     return mhi & ~mlo;
 }
-// exact native-domain sum (byte at absolute address a weighs 256^(a mod 4)) of
-// frame bytes [p0, p1) taken from a dword-aligned LDS image whose dword 0 is
-// frame-relative dword `d0` at byte `base` (slot: base = slot + 16, d0 = 0; stash: d0 = nd - 16).
-__device__ uint64_t nsum_lds(const char* lds, uint32_t base, int d0, int ndw, uint32_t sa, int p0, int p1) {
-    uint64_t s = 0;
+// sum, in the accumulator's 16-bit-half domain, of frame bytes [p0, p1) taken from a
+// dword-aligned LDS image whose dword 0 is frame-relative dword `d0` at byte `base`
+// (slot: base = slot + 16, d0 = 0; stash: d0 = nd - 16). Bytes outside the image count 0.
+__device__ uint32_t nsum_lds(const char* lds, uint32_t base, int d0, int ndw, uint32_t sa, int p0, int p1) {
+    uint32_t s = 0;
     if (p1 <= p0) return s;
     const int a0 = (int)sa + p0, a1 = (int)sa + p1;
     for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) {
         const int i = k - d0;
-        if (i >= 0 && i < ndw) s += lds32(lds, base + 4u * (uint32_t)i) & range_mask(k, a0, a1);
+        if (i >= 0 && i < ndw) s = sad16(lds32(lds, base + 4u * (uint32_t)i) & range_mask(k, a0, a1), s);
     }
     return s;
 }
@@ -246,15 +262,16 @@ struct Parsed {
     uint32_t stored;    // stored L4 checksum (BE)
     int compute;        // the L4 checksum is computed
     int parity;         // absolute parity of the L4 start (1 = odd)
-    uint32_t end;       // IP datagram end (frame-relative): Ethernet padding is [end, len)
-    int64_t corr;       // exact native-domain corrections except the padding
+    uint32_t off, end;  // L4 segment [off, end) (frame-relative); Ethernet padding is [end, len)
+    int64_t corr;       // checksum corrections except the padding (16-bit-half domain)
+    int64_t corr_fixed; // the pseudo-header and excluded-word part of corr
 };
 
 // Header parse for one frame (frame lane). Gates follow stacks/portstack.go:163-308
 // exactly (oracle/framesum_oracle.c restates them line by line; the parity tests
 // compare the two). Reads only the LDS header slot.
 __device__ Parsed parse_frame(const char* lds, uint32_t slot, uint32_t sa, uint32_t len, uint32_t mtu) {
-    Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0};
+    Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0};
     if (len < 34u) { r.verdict = V_SMOL; return r; }                          // portstack.go:167-168
     if (mtu != 0 && len > mtu) { r.verdict = V_MTU; return r; }              // :169-172
     uint32_t bs[9];                                                           // bswap32(frame dword j), j = 3..8
@@ -310,19 +327,21 @@ __device__ Parsed parse_frame(const char* lds, uint32_t slot, uint32_t sa, uint3
         return r;
     }
     r.compute = 1;
+    r.off = off;
     r.end = end;
-    // Native-domain total over [off, end) = streamed frame bytes >= P10 + these exact
-    // corrections (+ the padding correction applied at the end, from the stash).
+    // Total over [off, end) = streamed frame bytes >= P10 + these corrections (+ the padding
+    // correction applied at the end, from the stash), all in the 16-bit-half domain.
     const int P10 = 4 * kCsumRel0 - (int)sa;  // first streamed frame byte
     int64_t t = 0;
-    if ((int)off < P10) t += (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, (int)off, P10);
-    else t -= (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, P10, (int)off);
     t -= (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, (int)(off + excl),
                            (int)(off + excl + (proto == 6u ? 4u : 2u)));
     r.parity = (int)((sa + off) & 1u);
     const uint32_t w[6] = {bs[6] & 0xffffu, bs[7] >> 16, bs[7] & 0xffffu, bs[8] >> 16, proto, lenword};
 #pragma unroll
     for (int i = 0; i < 6; ++i) t += (int64_t)(r.parity ? w[i] : bswap16(w[i]));
+    r.corr_fixed = t;
+    if ((int)off < P10) t += (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, (int)off, P10);
+    else t -= (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, P10, (int)off);
     r.corr = t;
     return r;
 }
@@ -330,15 +349,25 @@ __device__ Parsed parse_frame(const char* lds, uint32_t slot, uint32_t sa, uint3
 // Final L4 checksum + verdict (frame lane) once the streamed sum is known.
 __device__ uint32_t finish_l4(const char* lds, uint32_t stash, const uint32_t* fb, uint32_t sa, uint32_t len,
                               uint32_t nd, const Parsed& P, uint64_t main_sum, uint32_t& verdict) {
-    int64_t t = (int64_t)main_sum + P.corr;
-    if (P.end < len) {  // Ethernet padding after the IP datagram
+    // Every term is congruent (mod 65535) to its exact native contribution, and the true
+    // total is > 0 (the pseudo-header protocol word is 6 or 17), so adding 65535 * 2^20
+    // keeps t positive and the fold below lands on the same one's-complement value.
+    int64_t t = (int64_t)main_sum + P.corr + 65535LL * (1LL << 20);
+    if (len >= (1u << 19)) {
+        // >= 512 KiB frame (only reachable with a huge Ethernet padding): a lane's streamed
+        // 32-bit sum may have wrapped, so sum the L4 segment [off, end) exactly from memory.
+        const int a0 = (int)(sa + P.off), a1 = (int)(sa + P.end);
+        uint32_t s = 0;
+        for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s = sad16(fb[k] & range_mask(k, a0, a1), s);
+        t = (int64_t)s + P.corr_fixed + 65535LL * (1LL << 20);
+    } else if (P.end < len) {  // Ethernet padding after the IP datagram
         const int sd0 = (int)nd - 16;
         if ((int)(sa + P.end) >= 4 * sd0) {
             t -= (int64_t)nsum_lds(lds, stash, sd0, 16, sa, (int)P.end, (int)len);
         } else {  // long padding (malformed frame): exact sum straight from global memory
             const int a0 = (int)(sa + P.end), a1 = (int)(sa + len);
-            uint64_t s = 0;
-            for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s += fb[k] & range_mask(k, a0, a1);
+            uint32_t s = 0;
+            for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s = sad16(fb[k] & range_mask(k, a0, a1), s);
             t -= (int64_t)s;
         }
     }
@@ -358,7 +387,8 @@ struct Tile {
     uint32_t fi, len, nd, sa, te;
     uint64_t E, sdw;
     // group lanes
-    int g_nd, R, Rp, Rsplit, rel0, rel_last, lo;
+    int g_nd, R, Rp, Rsplit, rel0, lo;
+    int RF_lo, RF_hi;  // wave-uniform rows where every lane takes the fast path
     uint32_t g_sa, g_te;
     const uint32_t* gfb;
 };
@@ -408,8 +438,22 @@ __device__ __forceinline__ void tile_geometry(Tile& T, uint64_t S, uint32_t lane
     rh = __builtin_amdgcn_readfirstlane(rh);
     T.Rsplit = min(T.Rp, (rh + kPrefetch) / kPrefetch * kPrefetch);
     T.rel0 = T.g_nd - kRowDwords * T.Rp + 4 * (int)gl;
-    T.rel_last = T.rel0 + kRowDwords * (T.Rp - 1);
     T.lo = (sdw_hi != 0 || sdw_lo > (1u << 24)) ? -(1 << 24) : -(int)sdw_lo;  // never below frames[0]
+    // Fast rows: rel in [kCsumRel0, nd - 5] (no head/tail/init masks, whole chunk streamed into
+    // the checksum); empty groups stream zeros and never force the slow path. Wave intersection.
+    int flo = -0x40000000, fhi = 0x40000000;
+    if (T.g_nd > 0) {
+        const int a = kCsumRel0 - T.rel0, b = T.g_nd - 5 - T.rel0;  // rows r with a <= 16 r <= b
+        flo = (a <= 0) ? 0 : (a + kRowDwords - 1) / kRowDwords;
+        fhi = (b < 0) ? -1 : b / kRowDwords;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        flo = max(flo, __shfl_xor(flo, m));
+        fhi = min(fhi, __shfl_xor(fhi, m));
+    }
+    T.RF_lo = __builtin_amdgcn_readfirstlane(flo);
+    T.RF_hi = __builtin_amdgcn_readfirstlane(fhi);
 }
 
 __global__ void __launch_bounds__(kThreads, 1)
@@ -490,14 +534,19 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         M.init1 = (1u << (8u * T.g_sa)) - 1u;
         M.tail_mask = (T.g_te == 4u) ? 0xffffffffu : ((1u << (8u * T.g_te)) - 1u);
 
-        // ---- main loop: rows 0..Rp-1, kPrefetch rows in flight, split at Rsplit for the header parse.
+        // ---- main loop: rows 0..Rp-1 with kPrefetch rows in flight, in three segments:
+        //   A [0, min(Rsplit, Rc))  capture the header rows into LDS, refill
+        //   B [.., Rc)              refill only
+        //   C [Rc, Rp)              the last kPrefetch rows: no refill (nothing past the frame end)
+        // The header parse runs between A and B (or after C when the header rows reach C),
+        // while the ring's loads are in flight.
         uint32_t A[4] = {0u, 0u, 0u, 0u};
-        Acc acc = {0u, 0u};
-        auto stream_rows = [&](int rbeg, int rend) {
+        uint32_t cs = 0u;
+        auto stream_rows = [&](int rbeg, int rend, auto hdr_tag, auto refill_tag) {
+            constexpr bool kHdr = decltype(hdr_tag)::value, kRefill = decltype(refill_tag)::value;
             for (int r0 = rbeg; r0 < rend; r0 += kPrefetch) {
                 // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
-                // so without this the youngest of a SIMD's 4 waves finishes last and sets
-                // the kernel time. A wave with more rows left gets a higher priority.
+                // a wave with more rows left gets a higher priority.
                 if (FS_PRIO) {
                     const int left4 = (4 * (T.Rp - r0)) / max(T.Rp, 1);  // 4 .. 1
                     if (left4 >= 4) __builtin_amdgcn_s_setprio(3);
@@ -507,24 +556,34 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
                 }
 #pragma unroll
                 for (int i = 0; i < kPrefetch; ++i) {
-                    const int rel = T.rel0 + kRowDwords * (r0 + i);
-                    const bool lane_fast = rel >= M.fast_lo && rel <= M.fast_hi;
-                    const bool fast = __all(lane_fast);
+                    const int r = r0 + i;
+                    const int rel = T.rel0 + kRowDwords * r;
+                    const bool fast = (r >= T.RF_lo) && (r <= T.RF_hi);  // wave-uniform (scalar)
+                    if (kHdr) capture_header(lds, gslot, rel, T.lo, pf[i]);
                     // consume the ring slot, then refill the SAME registers: no copy of an
                     // in-flight load, so the compiler keeps kPrefetch-1 loads outstanding
-                    process_row(lds, keys, pf[i], rel, fast, M, T.lo, gslot, A, acc);
-                    if (FS_DIAG != 3) pf[i] = load_chunk(T.gfb, min(rel + kRowDwords * kPrefetch, T.rel_last), T.lo);
+                    process_row(lds, keys, pf[i], rel, fast, M, T.lo, A, cs);
+                    if (kRefill && FS_DIAG != 3) pf[i] = load_chunk(T.gfb, rel + kRowDwords * kPrefetch, T.lo);
                 }
             }
         };
-        stream_rows(0, T.Rsplit);
-        // header parse while the next kPrefetch rows are in flight
-        Parsed P = {V_OK, 0u, 0u, 0, 0, 0u, 0};
-        if (T.fvalid) P = parse_frame(lds, slot, T.sa, T.len, mtu);
-        stream_rows(T.Rsplit, T.Rp);
+        using Yes = std::true_type;
+        using No = std::false_type;
+        Parsed P = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0};
+        const int Rc = T.Rp - kPrefetch;
+        if (T.Rp > 0) {
+            const int ra = min(T.Rsplit, Rc);
+            stream_rows(0, ra, Yes(), Yes());
+            if (T.Rsplit <= Rc && T.fvalid) P = parse_frame(lds, slot, T.sa, T.len, mtu);
+            stream_rows(ra, Rc, No(), Yes());
+            stream_rows(Rc, T.Rp, Yes(), No());
+            if (T.Rsplit > Rc && T.fvalid) P = parse_frame(lds, slot, T.sa, T.len, mtu);
+        } else if (T.fvalid) {
+            P = parse_frame(lds, slot, T.sa, T.len, mtu);  // only sub-4-byte frames: rejected by len
+        }
         FS_STAMP(2);
-        // the refills of the last rows all re-read the final row: stash it for the padding sum
-        *reinterpret_cast<u32x4*>(lds + stash_base + grp * kStashBytes + 16u * gl) = pf[0];
+        // the last ring slot holds the frame's final row: stash it for the padding sum
+        *reinterpret_cast<u32x4*>(lds + stash_base + grp * kStashBytes + 16u * gl) = pf[kPrefetch - 1];
 
         // ---- combine the 16 streams of each frame: C = Z_(4-t)( xor_l Z_16(3-l)( U_l ) ),
         //      U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3   (3 dependent LDS round trips).
@@ -536,17 +595,12 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         Y ^= dpp_quad<kQuadXor2>(Y);
         const uint32_t tpad = (4u - T.g_te) & 3u;  // zero bytes appended by the dword rounding
         const uint32_t C = zplain(lds, Y, kLdsZfin + 4096u * tpad);
-        uint64_t cs = ((uint64_t)acc.hi << 32) | acc.lo;
-        {   // 64-bit sum over the 4 lanes of the group
-            uint64_t t = ((uint64_t)dpp_quad<kQuadXor1>(acc.hi) << 32) | dpp_quad<kQuadXor1>(acc.lo);
-            cs += t;
-            t = ((uint64_t)dpp_quad<kQuadXor2>((uint32_t)(cs >> 32)) << 32) | dpp_quad<kQuadXor2>((uint32_t)cs);
-            cs += t;
-        }
+        // checksum partial sum over the 4 lanes of the group (each < 2^30: no u32 overflow)
+        cs += dpp_quad<kQuadXor1>(cs);
+        cs += dpp_quad<kQuadXor2>(cs);
         const uint32_t src = (lane & 15u) * 4u;
         uint32_t crcv = (uint32_t)__shfl((int)C, (int)src);
-        const uint64_t csum = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cs >> 32), (int)src) << 32) |
-                              (uint32_t)__shfl((int)(uint32_t)cs, (int)src);
+        const uint64_t csum = (uint32_t)__shfl((int)cs, (int)src);
 
         FS_STAMP(3);
         // ---- frame lanes: finish and store.

@@ -139,6 +139,22 @@ def test_random_lengths_large(engine):
     check(engine, buf, off, ln, label="random")
 
 
+def test_giant_padded_frame(engine):
+    # A >= 512 KiB frame whose IP datagram is short: RecvEth still checksums [off, end) and the
+    # rest is Ethernet padding (the kernel's exact-from-memory fallback for huge frames).
+    import random
+    import framegen
+
+    rnd = random.Random(8)
+    frames = []
+    for L, pad in ((1000, 600000), (1400, 700001), (200, 3)):
+        f = framegen.valid_frame(rnd, 6 if L != 200 else 17, payload=L, pad=pad)
+        frames.append(f)
+    frames.append(bytes(rnd.randbytes(530000)))  # giant non-IP frame: CRC only
+    buf, off, ln = pack_frames(frames, align=1)
+    check(engine, buf, off, ln, label="giant")
+
+
 def test_corruption_detected(engine):
     buf, off, ln = synth.uniform_batch(4096, 1500, seed=9)
     rng = np.random.default_rng(1)
