@@ -47,7 +47,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 #ifndef FS_PREFETCH
-#define FS_PREFETCH 4
+#define FS_PREFETCH 6
+#endif
+#ifndef FS_DMA_FIRST
+#define FS_DMA_FIRST 1  // 1: table LDS-DMA before the descriptors (ahead of the first rows)
 #endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio in the row loop (see stream_rows)
@@ -63,8 +66,11 @@ constexpr int kFramesPerTile = 16;
 constexpr int kRowDwords = 16;
 constexpr int kPrefetch = FS_PREFETCH;
 constexpr int kHdrDwords = 28;              // frame bytes [0, 112) staged for the header parse
-constexpr int kHdrSlotBytes = 16 + 4 * kHdrDwords;  // + a 16-B guard for chunks that start before the frame
-constexpr int kStashBytes = 64;             // the frame's last row (Ethernet padding source)
+// + a 16-B guard for chunks that start before the frame, + 8 B so consecutive slots are 34 dwords
+// apart: the 16 frame lanes reading dword k of their slots hit 16 distinct banks (ds_read_b32
+// banks are (a/4) mod 32; a 32-dword stride made every parse read a 16-way conflict)
+constexpr int kHdrSlotBytes = 16 + 4 * kHdrDwords + 8;
+constexpr int kStashBytes = 68;             // the frame's last row (Ethernet padding source); 17-dword stride
 constexpr int kCsumRel0 = 10;               // streamed checksum starts at frame dword 10
 
 // LDS map (bytes). [0, 88 KB) is FsTables verbatim (filled by LDS-DMA).
@@ -86,16 +92,24 @@ constexpr uint32_t kDmaPerWave = (kTableChunks + kWavesPerBlock - 1) / kWavesPer
 
 #ifdef FS_STAMPS
 // Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
-__device__ unsigned long long g_fs_stamps[8192 * 8];
+__device__ unsigned long long g_fs_stamps[8192 * 16];
 #define FS_STAMP(k)                                                                          \
     do {                                                                                     \
         __builtin_amdgcn_sched_barrier(0);                                                   \
         unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
-        if (lane == 0 && gwave < 8192u) g_fs_stamps[gwave * 8u + (k)] = t_;                  \
+        if (lane == 0 && gwave < 8192u) g_fs_stamps[gwave * 16u + (k)] = t_;                  \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+    } while (0)
+#define FS_RTSTAMP(k)                                                                        \
+    do {                                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+        unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                            \
+        if (lane == 0 && gwave < 8192u) g_fs_stamps[gwave * 16u + (k)] = t_;                  \
         __builtin_amdgcn_sched_barrier(0);                                                   \
     } while (0)
 #else
 #define FS_STAMP(k) do { } while (0)
+#define FS_RTSTAMP(k) do { } while (0)
 #endif
 
 constexpr uint32_t kZ4Off = 128;  // Z4 copies sit in slots 32..63 of each region-A entry row
@@ -111,9 +125,6 @@ enum : uint32_t {
 
 __device__ __forceinline__ uint32_t lds32(const char* lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t*>(lds + byte_addr);
-}
-__device__ __forceinline__ uint32_t lds8(const char* lds, uint32_t byte_addr) {
-    return *reinterpret_cast<const uint8_t*>(lds + byte_addr);
 }
 
 struct LaneKeys {
@@ -153,8 +164,8 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xffu) <<
 // 16 bytes of row data for one lane: dwords [rel, rel+4) relative to the frame's
 // first dword. Issued unconditionally (no divergent branch around the load, so
 // the prefetch ring keeps kPrefetch-1 loads in flight); rows that start before
-// the frame are clamped to `lo` (>= the buffer start) and fixed up / masked by
-// the slow path. Rows never run past the frame's last dword (see the segments).
+// the frame are clamped to `lo` (the frame's first chunk, never below the buffer
+// start) and realigned / masked by the slow path. Rows never run past the frame's last dword (see the segments).
 __device__ __forceinline__ u32x4 load_chunk(const uint32_t* fb, int rel, int lo) {
     return *reinterpret_cast<const u32x4_a4*>(fb + max(rel, lo));
 }
@@ -189,7 +200,7 @@ __device__ __forceinline__ void process_row(char* lds, const LaneKeys& keys, u32
         cs = sad16(v.z, cs);
         cs = sad16(v.w, cs);
     } else {
-        const int sh = max(rel, lo) - rel;  // >0 only when the load was clamped at the buffer start
+        const int sh = max(rel, lo) - rel;  // >0 only for a clamped row that starts before the frame
         if (sh > 0 && sh < 4) {
             const u32x4 u = v;
             v.w = (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
@@ -216,7 +227,7 @@ __device__ __forceinline__ void process_row(char* lds, const LaneKeys& keys, u32
 __device__ __forceinline__ void capture_header(char* lds, uint32_t hdr_slot, int rel, int lo, u32x4 v) {
     if (rel > -4 && rel < kHdrDwords) {
         const int sh = max(rel, lo) - rel;
-        if (sh > 0 && sh < 4) {  // clamped load at the buffer start: realign as process_row does
+        if (sh > 0 && sh < 4) {  // clamped load: realign as process_row does
             const u32x4 u = v;
             v.w = (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
             v.z = (sh == 1) ? u.y : (sh == 2) ? u.x : 0u;
@@ -380,24 +391,23 @@ __device__ uint32_t finish_l4(const char* lds, uint32_t stash, const uint32_t* f
     return l4;
 }
 
-// Per-tile state of one wave.
+// Per-tile state of one wave. Every lane describes its GROUP's frame (the 4 lanes of a
+// group load the same descriptor; the group's lane 0 parses, finishes and stores it),
+// so no lane-to-lane broadcast is needed anywhere on the tile's critical path.
 struct Tile {
-    // frame lane (lanes 0..15)
     bool fvalid;
     uint32_t fi, len, nd, sa, te;
     uint64_t E, sdw;
-    // group lanes
-    int g_nd, R, Rp, Rsplit, rel0, lo;
+    int R, Rp, Rsplit, rel0, lo;
     int RF_lo, RF_hi;  // wave-uniform rows where every lane takes the fast path
-    uint32_t g_sa, g_te;
     const uint32_t* gfb;
 };
 
-__device__ __forceinline__ void tile_descriptors(Tile& T, uint32_t tile, uint32_t lane, uint32_t n,
+__device__ __forceinline__ void tile_descriptors(Tile& T, uint32_t tile, uint32_t grp, uint32_t n,
                                                  const uint64_t* __restrict__ offsets,
                                                  const uint32_t* __restrict__ lengths, uint64_t& S) {
-    T.fi = tile * kFramesPerTile + lane;
-    T.fvalid = lane < (uint32_t)kFramesPerTile && T.fi < n;
+    T.fi = tile * kFramesPerTile + grp;
+    T.fvalid = T.fi < n;
     S = 0;
     T.len = 0;
     if (T.fvalid) {
@@ -406,54 +416,65 @@ __device__ __forceinline__ void tile_descriptors(Tile& T, uint32_t tile, uint32_
     }
 }
 
-__device__ __forceinline__ void tile_geometry(Tile& T, uint64_t S, uint32_t lane, uint32_t grp, uint32_t gl,
-                                              const uint8_t* __restrict__ frames) {
+// Wave max / min of a value that is uniform within each 4-lane group: two DPP row
+// mirrors combine the 4 groups of a 16-lane row, 4 readlanes the rows (no LDS permutes).
+template <bool kMax>
+__device__ __forceinline__ int group_reduce(int x) {
+    int y = __builtin_amdgcn_mov_dpp(x, 0x140, 0xf, 0xf, false);  // row_mirror
+    x = kMax ? max(x, y) : min(x, y);
+    y = __builtin_amdgcn_mov_dpp(x, 0x141, 0xf, 0xf, false);      // row_half_mirror
+    x = kMax ? max(x, y) : min(x, y);
+    const int a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
+    const int c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
+    return kMax ? max(max(a, b), max(c, d)) : min(min(a, b), min(c, d));
+}
+
+__device__ __forceinline__ void tile_geometry(Tile& T, uint64_t S, uint32_t gl, const uint8_t* __restrict__ frames) {
     T.E = S + T.len;
     T.sdw = S >> 2;
     const uint32_t ndall = (uint32_t)(((T.E + 3u) >> 2) - T.sdw);
     T.nd = (T.fvalid && T.len >= 4u) ? ndall : 0u;
     T.sa = (uint32_t)(S & 3u);
     T.te = (uint32_t)(T.E & 3u) ? (uint32_t)(T.E & 3u) : 4u;
-    // group lanes (rebuilt from the kernel argument so loads stay global_load, not flat_load)
-    const uint32_t sdw_lo = (uint32_t)__shfl((int)(uint32_t)T.sdw, (int)grp);
-    const uint32_t sdw_hi = (uint32_t)__shfl((int)(uint32_t)(T.sdw >> 32), (int)grp);
-    T.gfb = reinterpret_cast<const uint32_t*>(frames + ((((uint64_t)sdw_hi << 32) | sdw_lo) << 2));
-    T.g_nd = __shfl((int)T.nd, (int)grp);
-    T.g_sa = (uint32_t)__shfl((int)T.sa, (int)grp);
-    T.g_te = (uint32_t)__shfl((int)T.te, (int)grp);
-    uint32_t rows = (lane < (uint32_t)kFramesPerTile) ? (T.nd + kRowDwords - 1) / kRowDwords : 0u;
-#pragma unroll
-    for (int m = 8; m >= 1; m >>= 1) rows = max(rows, (uint32_t)__shfl_xor((int)rows, m));
-    T.R = __builtin_amdgcn_readfirstlane((int)rows);
+    T.gfb = reinterpret_cast<const uint32_t*>(frames + (T.sdw << 2));
+    const int nd = (int)T.nd;
+    T.R = group_reduce<true>((nd + kRowDwords - 1) / kRowDwords);
     // Rows padded at the FRONT to a multiple of kPrefetch: leading all-zero rows
     // leave a zero-init CRC stream unchanged, so the loop needs no tail guard.
     T.Rp = (T.R + kPrefetch - 1) / kPrefetch * kPrefetch;
+    const int base0 = nd - kRowDwords * T.Rp;  // rel of the group's lane 0 in row 0
+    T.rel0 = base0 + 4 * (int)gl;
     // Rsplit: first row (multiple of kPrefetch) by which every frame's header dwords
     // [0, 28) have streamed through the slot; the header parse runs there.
-    int rh = -1;
-    if (lane < (uint32_t)kFramesPerTile && T.nd > 0)
-        rh = (min(kHdrDwords - 1, (int)T.nd - 1) - ((int)T.nd - kRowDwords * T.Rp)) / kRowDwords;
-#pragma unroll
-    for (int m = 8; m >= 1; m >>= 1) rh = max(rh, __shfl_xor(rh, m));
-    rh = __builtin_amdgcn_readfirstlane(rh);
+    const int rh = group_reduce<true>(nd > 0 ? (min(kHdrDwords - 1, nd - 1) - base0) / kRowDwords : -1);
     T.Rsplit = min(T.Rp, (rh + kPrefetch) / kPrefetch * kPrefetch);
-    T.rel0 = T.g_nd - kRowDwords * T.Rp + 4 * (int)gl;
-    T.lo = (sdw_hi != 0 || sdw_lo > (1u << 24)) ? -(1 << 24) : -(int)sdw_lo;  // never below frames[0]
-    // Fast rows: rel in [kCsumRel0, nd - 5] (no head/tail/init masks, whole chunk streamed into
-    // the checksum); empty groups stream zeros and never force the slow path. Wave intersection.
+    // Loads of rows that start before the frame are clamped to the frame's first chunk (its last
+    // chunk for frames under 4 dwords), so lanes idling through a tile's longest frame re-read
+    // one cached line instead of fetching the bytes that precede their frame; never below frames[0].
+    T.lo = max(T.sdw > (1u << 24) ? -(1 << 24) : -(int)T.sdw, min(0, nd - 4));
+    // Fast rows: every lane's chunk [rel, rel+4) inside [kCsumRel0, nd - 1) (no head/tail/init
+    // masks, whole chunk streamed into the checksum): lane 0 of the group bounds the start,
+    // lane 3 the end. Empty groups stream zeros and never force the slow path.
     int flo = -0x40000000, fhi = 0x40000000;
-    if (T.g_nd > 0) {
-        const int a = kCsumRel0 - T.rel0, b = T.g_nd - 5 - T.rel0;  // rows r with a <= 16 r <= b
+    if (nd > 0) {
+        const int a = kCsumRel0 - base0, b = nd - 5 - (base0 + 12);  // rows r with a <= 16 r <= b
         flo = (a <= 0) ? 0 : (a + kRowDwords - 1) / kRowDwords;
         fhi = (b < 0) ? -1 : b / kRowDwords;
     }
+    T.RF_lo = group_reduce<true>(flo);
+    T.RF_hi = group_reduce<false>(fhi);
+}
+
+// The tables' LDS image by LDS-DMA: exactly kDmaPerWave 1-KB pieces per wave (a static
+// count; surplus pieces re-copy the last chunk with identical bytes).
+__device__ __forceinline__ void table_dma(const FsTables* __restrict__ tabs, char* lds, uint32_t wave, uint32_t lane) {
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        flo = max(flo, __shfl_xor(flo, m));
-        fhi = min(fhi, __shfl_xor(fhi, m));
+    for (uint32_t k = 0; k < (FS_DIAG == 4 ? 0u : kDmaPerWave); ++k) {
+        const uint32_t c = min(w0 + k * kWavesPerBlock, kTableChunks - 1u);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
+                                         lds + c * 1024u, 16, 0, 0);
     }
-    T.RF_lo = __builtin_amdgcn_readfirstlane(flo);
-    T.RF_hi = __builtin_amdgcn_readfirstlane(fhi);
 }
 
 __global__ void __launch_bounds__(kThreads, 1)
@@ -472,9 +493,8 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     const uint32_t hdr_base = kLdsHdr + wave * (kFramesPerTile * kHdrSlotBytes);
     const uint32_t stash_base = kLdsStash + wave * (kFramesPerTile * kStashBytes);
 
-    const uint32_t slot = hdr_base + (lane & 15u) * kHdrSlotBytes;       // frame lane's slot
-    const uint32_t gslot = hdr_base + grp * kHdrSlotBytes;               // group's slot
-    const uint32_t stash = stash_base + (lane & 15u) * kStashBytes;      // frame lane's last-row stash
+    const uint32_t gslot = hdr_base + grp * kHdrSlotBytes;      // the group's header slot
+    const uint32_t stash = stash_base + grp * kStashBytes;      // the group's last-row stash
     LaneKeys keys;
     {
         const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
@@ -488,51 +508,58 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         }
     }
 
-    // Preamble, ordered so that only ONE memory round trip precedes the first row's
-    // load: the table LDS-DMA and the first tile's descriptors are issued back to back
-    // (hipcc does not count LDS-DMA in its vmcnt model, so the descriptors go last),
-    // then the row prefetch; the tables are waited for just before the first lookup.
+    // Preamble: the first tile's descriptors (one round trip), its geometry, the row
+    // prefetch, and only THEN the table LDS-DMA, so that the CU's in-order vector-memory
+    // queue serves the descriptors and the first rows before the 100 KB of table pieces;
+    // the DMA (L2 hits) then overlaps the rows' HBM latency. hipcc does not count LDS-DMA
+    // in its vmcnt model: the DMA is issued last and drained with an explicit vmcnt(0),
+    // which the first row needs anyway.
     uint32_t tile = gwave;
+    FS_RTSTAMP(5);
     FS_STAMP(0);
     Tile T;
     uint64_t S;
     u32x4 pf[kPrefetch];
-    {   // exactly kDmaPerWave pieces per wave (a static count keeps the compiler's vmcnt
-        // bookkeeping exact); surplus pieces re-copy the last chunk with identical bytes
-        const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-        for (uint32_t k = 0; k < (FS_DIAG == 4 ? 0u : kDmaPerWave); ++k) {
-            const uint32_t c = min(w0 + k * kWavesPerBlock, kTableChunks - 1u);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
-                                             lds + c * 1024u, 16, 0, 0);
-        }
-    }
-    tile_descriptors(T, tile, lane, n, offsets, lengths, S);  // after the DMA: one shared round trip
+#if FS_DMA_FIRST
+    table_dma(tabs, lds, wave, lane);
+#endif
+    tile_descriptors(T, tile, grp, n, offsets, lengths, S);
+#if defined(FS_STAMPS) && FS_STAMPS == 2
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // fine-stamp build only: time the descriptor round trip
+    FS_STAMP(8);
+#endif
     if (__builtin_amdgcn_readfirstlane(tile) < ntiles) {
-        tile_geometry(T, S, lane, grp, gl, frames);
+        tile_geometry(T, S, gl, frames);
 #pragma unroll
         for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
-        __builtin_amdgcn_s_waitcnt(0x0f70 | kPrefetch);  // vmcnt(kPrefetch): the table pieces are older
-    } else {
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     }
+    FS_STAMP(9);
+#if !FS_DMA_FIRST
+    table_dma(tabs, lds, wave, lane);
+#endif
+#if FS_DMA_FIRST
+    __builtin_amdgcn_s_waitcnt(0x0f70 | kPrefetch);  // vmcnt(kPrefetch): the table pieces are older
+#else
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): table pieces and the first rows
+#endif
+    FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // LDS tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     FS_STAMP(1);
 
     while (tile < ntiles) {
         RowMasks M;
-        M.nd = T.g_nd;
-        if (T.g_nd > 0) {
+        M.nd = (int)T.nd;
+        if (T.nd > 0) {
             M.fast_lo = kCsumRel0;
-            M.fast_hi = T.g_nd - 5;
+            M.fast_hi = (int)T.nd - 5;
         } else {  // empty group: every row streams zeros
             M.fast_lo = -0x40000000;
             M.fast_hi = 0x40000000;
         }
-        M.head_mask = 0xffffffffu << (8u * T.g_sa);
+        M.head_mask = 0xffffffffu << (8u * T.sa);
         M.init0 = M.head_mask;
-        M.init1 = (1u << (8u * T.g_sa)) - 1u;
-        M.tail_mask = (T.g_te == 4u) ? 0xffffffffu : ((1u << (8u * T.g_te)) - 1u);
+        M.init1 = (1u << (8u * T.sa)) - 1u;
+        M.tail_mask = (T.te == 4u) ? 0xffffffffu : ((1u << (8u * T.te)) - 1u);
 
         // ---- main loop: rows 0..Rp-1 with kPrefetch rows in flight, in three segments:
         //   A [0, min(Rsplit, Rc))  capture the header rows into LDS, refill
@@ -570,20 +597,21 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         using Yes = std::true_type;
         using No = std::false_type;
         Parsed P = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0};
+        const bool parser = T.fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
         const int Rc = T.Rp - kPrefetch;
         if (T.Rp > 0) {
             const int ra = min(T.Rsplit, Rc);
             stream_rows(0, ra, Yes(), Yes());
-            if (T.Rsplit <= Rc && T.fvalid) P = parse_frame(lds, slot, T.sa, T.len, mtu);
+            if (T.Rsplit <= Rc && parser) P = parse_frame(lds, gslot, T.sa, T.len, mtu);
             stream_rows(ra, Rc, No(), Yes());
             stream_rows(Rc, T.Rp, Yes(), No());
-            if (T.Rsplit > Rc && T.fvalid) P = parse_frame(lds, slot, T.sa, T.len, mtu);
-        } else if (T.fvalid) {
-            P = parse_frame(lds, slot, T.sa, T.len, mtu);  // only sub-4-byte frames: rejected by len
+            if (T.Rsplit > Rc && parser) P = parse_frame(lds, gslot, T.sa, T.len, mtu);
+        } else if (parser) {
+            P = parse_frame(lds, gslot, T.sa, T.len, mtu);  // only sub-4-byte frames: rejected by len
         }
         FS_STAMP(2);
         // the last ring slot holds the frame's final row: stash it for the padding sum
-        *reinterpret_cast<u32x4*>(lds + stash_base + grp * kStashBytes + 16u * gl) = pf[kPrefetch - 1];
+        *reinterpret_cast<u32x4*>(lds + stash + 16u * gl) = pf[kPrefetch - 1];
 
         // ---- combine the 16 streams of each frame: C = Z_(4-t)( xor_l Z_16(3-l)( U_l ) ),
         //      U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3   (3 dependent LDS round trips).
@@ -593,18 +621,17 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         if (gl == 3u) Y = U;
         Y ^= dpp_quad<kQuadXor1>(Y);
         Y ^= dpp_quad<kQuadXor2>(Y);
-        const uint32_t tpad = (4u - T.g_te) & 3u;  // zero bytes appended by the dword rounding
+        const uint32_t tpad = (4u - T.te) & 3u;  // zero bytes appended by the dword rounding
         const uint32_t C = zplain(lds, Y, kLdsZfin + 4096u * tpad);
         // checksum partial sum over the 4 lanes of the group (each < 2^30: no u32 overflow)
         cs += dpp_quad<kQuadXor1>(cs);
         cs += dpp_quad<kQuadXor2>(cs);
-        const uint32_t src = (lane & 15u) * 4u;
-        uint32_t crcv = (uint32_t)__shfl((int)C, (int)src);
-        const uint64_t csum = (uint32_t)__shfl((int)cs, (int)src);
+        uint32_t crcv = C;
+        const uint64_t csum = cs;
 
         FS_STAMP(3);
-        // ---- frame lanes: finish and store.
-        if (T.fvalid) {
+        // ---- the group's lane 0: finish and store.
+        if (parser) {
             if (T.len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
                 uint32_t c = 0xffffffffu;
                 const uint8_t* fbytes = frames + T.E - T.len;
@@ -623,10 +650,11 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
             if (status) status[T.fi] = (uint8_t)verdict;
         }
         FS_STAMP(4);
+        FS_RTSTAMP(6);
         tile += nwaves;
         if (tile < ntiles) {  // next tile: descriptors, geometry, row prefetch
-            tile_descriptors(T, tile, lane, n, offsets, lengths, S);
-            tile_geometry(T, S, lane, grp, gl, frames);
+            tile_descriptors(T, tile, grp, n, offsets, lengths, S);
+            tile_geometry(T, S, gl, frames);
 #pragma unroll
             for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
         }

@@ -28,11 +28,11 @@ st = torch.empty((a.frames,), dtype=torch.uint8, device=dev)
 for i in range(8):
     e.digest_device(*bs[i % 4], out=out, status=st)
 torch.cuda.synchronize()
-arr = np.zeros(8192 * 8, dtype=np.uint64)
+arr = np.zeros(8192 * 16, dtype=np.uint64)
 rc = e.lib.fs_debug_read_stamps(arr.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(arr.nbytes))
 assert rc == 0, rc
 nw = min(8192, (a.frames + 15) // 16)
-s = arr.reshape(8192, 8)[:nw].astype(np.int64)
+s = arr.reshape(8192, 16)[:nw].astype(np.int64)
 names = ["fill+desc->sync", "main loop", "combine", "finalize"]
 print(f"waves={nw}  (cycles, s_memtime ticks)")
 for k, nm in enumerate(names):
@@ -47,3 +47,18 @@ print("  main loop median by wave-in-block:", [int(np.median(ml[(np.arange(nw) %
 st = s[:, 0] - s[:, 0].min()
 print("  start skew (ticks) p50/p90/max:", int(np.median(st)), int(np.percentile(st, 90)), int(st.max()))
 print(f"  {'wave total':18s} median {int(np.median(tot)):8d}  p10 {int(np.percentile(tot, 10)):8d}  p90 {int(np.percentile(tot, 90)):8d}")
+# s_memrealtime (100 MHz, chip-wide) timeline: launch ramp and tail, in microseconds
+rs, re_ = s[:, 5], s[:, 6]
+t0 = rs.min()
+us = lambda x: x * 0.01  # noqa: E731
+print(f"  realtime: span {us(re_.max() - t0):.2f} us; wave start offset p50/p90/max "
+      f"{us(np.median(rs - t0)):.2f}/{us(np.percentile(rs - t0, 90)):.2f}/{us((rs - t0).max()):.2f} us; "
+      f"wave end p10/p50/p90/max {us(np.percentile(re_ - t0, 10)):.2f}/{us(np.median(re_ - t0)):.2f}/"
+      f"{us(np.percentile(re_ - t0, 90)):.2f}/{us((re_ - t0).max()):.2f} us")
+print(f"  memtime ticks per us (median over waves): {np.median((s[:, 4] - s[:, 0]) / np.maximum(1, us(re_ - rs))):.0f}")
+if s[:, 9].any():
+    for nm, a_, b_ in (("start->desc (fine)", 0, 8), ("desc->geom+issue", 8, 9), ("start->geom+issue", 0, 9),
+                       ("issue->waitcnt", 9, 10), ("waitcnt->barrier", 10, 1)):
+        if s[:, b_].any() and s[:, a_].any():
+            d = s[:, b_] - s[:, a_]
+            print(f"  {nm:18s} median {int(np.median(d)):8d}  p10 {int(np.percentile(d, 10)):8d}  p90 {int(np.percentile(d, 90)):8d}")
