@@ -13,12 +13,19 @@
 
 using framesum::FsTables;
 
-struct fs_ctx {
-    int device = 0;
-    int num_cus = 0;
-    FsTables* d_tables = nullptr;
-    hipStream_t stream = nullptr;
-    // host-staged path: grow-only device buffers
+// Host-staged path: the batch is cut into chunks of about kChunkBytes of frame bytes,
+// staged through kHostSlots device buffers. All H2D copies go back to back on one copy
+// stream (one DMA engine streaming the PCIe link); kernels and the small D2H copies run
+// on a compute stream. Events order each chunk's kernel after its copy (`copied`) and
+// the reuse of a slot by chunk c + kHostSlots after chunk c's kernel (`consumed`), so
+// chunk c+1's H2D overlaps chunk c's kernel and D2H.
+constexpr int kHostSlots = 3;
+constexpr uint64_t kChunkBytes = 16ull << 20;
+constexpr uint32_t kChunkFrames = 1u << 20;
+
+struct HostSlot {
+    hipEvent_t copied = nullptr, consumed = nullptr;
+    bool used = false;
     uint8_t* d_frames = nullptr;
     uint64_t cap_frames = 0;
     uint64_t* d_offsets = nullptr;
@@ -26,6 +33,18 @@ struct fs_ctx {
     fs_digest* d_out = nullptr;
     uint8_t* d_status = nullptr;
     uint32_t cap_n = 0;
+};
+
+struct fs_ctx {
+    int device = 0;
+    int num_cus = 0;
+    FsTables* d_tables = nullptr;
+    HostSlot slot[kHostSlots];
+    hipStream_t copy_stream = nullptr, compute_stream = nullptr;
+    // pinned host mirrors of the descriptors and results, so every per-chunk copy is
+    // asynchronous even when the caller's arrays are pageable (Go slices, numpy)
+    uint8_t* h_pin = nullptr;
+    uint64_t cap_pin_n = 0;
     std::string err;
 };
 
@@ -49,32 +68,45 @@ fs_status hip_err(fs_ctx* ctx, hipError_t e, const char* what) {
         if (e_ != hipSuccess) return hip_err(ctx, e_, #call); \
     } while (0)
 
-fs_status ensure_staging(fs_ctx* ctx, uint64_t frames_bytes, uint32_t n) {
-    if (frames_bytes > ctx->cap_frames) {
-        if (ctx->d_frames) (void)hipFree(ctx->d_frames);
-        ctx->d_frames = nullptr;
-        ctx->cap_frames = 0;
-        uint64_t cap = frames_bytes + 256;
-        if (hipMalloc(&ctx->d_frames, cap) != hipSuccess) return set_err(ctx, FS_E_NOMEM, "hipMalloc frames staging");
-        ctx->cap_frames = cap;
+// Grow-only staging of one slot; a slot being regrown first waits for its last kernel.
+fs_status ensure_slot(fs_ctx* ctx, HostSlot& sl, uint64_t frame_bytes, uint32_t n) {
+    if (frame_bytes > sl.cap_frames) {
+        if (sl.used) FS_HIP(ctx, hipEventSynchronize(sl.consumed));
+        (void)hipFree(sl.d_frames);
+        sl.d_frames = nullptr;
+        sl.cap_frames = 0;
+        const uint64_t cap = frame_bytes + 256;
+        if (hipMalloc(&sl.d_frames, cap) != hipSuccess) return set_err(ctx, FS_E_NOMEM, "hipMalloc frames staging");
+        sl.cap_frames = cap;
     }
-    if (n > ctx->cap_n) {
-        (void)hipFree(ctx->d_offsets);
-        (void)hipFree(ctx->d_lengths);
-        (void)hipFree(ctx->d_out);
-        (void)hipFree(ctx->d_status);
-        ctx->d_offsets = nullptr;
-        ctx->d_lengths = nullptr;
-        ctx->d_out = nullptr;
-        ctx->d_status = nullptr;
-        ctx->cap_n = 0;
-        if (hipMalloc(&ctx->d_offsets, (size_t)n * 8) != hipSuccess ||
-            hipMalloc(&ctx->d_lengths, (size_t)n * 4) != hipSuccess ||
-            hipMalloc(&ctx->d_out, (size_t)n * sizeof(fs_digest)) != hipSuccess ||
-            hipMalloc(&ctx->d_status, (size_t)n) != hipSuccess)
+    if (n > sl.cap_n) {
+        if (sl.used) FS_HIP(ctx, hipEventSynchronize(sl.consumed));
+        (void)hipFree(sl.d_offsets);
+        (void)hipFree(sl.d_lengths);
+        (void)hipFree(sl.d_out);
+        (void)hipFree(sl.d_status);
+        sl.d_offsets = nullptr;
+        sl.d_lengths = nullptr;
+        sl.d_out = nullptr;
+        sl.d_status = nullptr;
+        sl.cap_n = 0;
+        if (hipMalloc(&sl.d_offsets, (size_t)n * 8) != hipSuccess || hipMalloc(&sl.d_lengths, (size_t)n * 4) != hipSuccess ||
+            hipMalloc(&sl.d_out, (size_t)n * sizeof(fs_digest)) != hipSuccess || hipMalloc(&sl.d_status, (size_t)n) != hipSuccess)
             return set_err(ctx, FS_E_NOMEM, "hipMalloc descriptor staging");
-        ctx->cap_n = n;
+        sl.cap_n = n;
     }
+    return FS_SUCCESS;
+}
+
+// h_pin layout for n frames: offsets (8n) | lengths (4n) | digests (8n) | status (n)
+fs_status ensure_pinned(fs_ctx* ctx, uint32_t n) {
+    if (n <= ctx->cap_pin_n) return FS_SUCCESS;
+    if (ctx->h_pin) FS_HIP(ctx, hipHostFree(ctx->h_pin));
+    ctx->h_pin = nullptr;
+    ctx->cap_pin_n = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pin), (size_t)n * 21 + 64, hipHostMallocDefault) != hipSuccess)
+        return set_err(ctx, FS_E_NOMEM, "hipHostMalloc descriptor mirror");
+    ctx->cap_pin_n = n;
     return FS_SUCCESS;
 }
 
@@ -116,7 +148,12 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
     framesum::build_tables(h);
     e = hipMalloc(&ctx->d_tables, sizeof(FsTables));
     if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, h, sizeof(FsTables), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->compute_stream, hipStreamNonBlocking);
+    for (int k = 0; k < kHostSlots && e == hipSuccess; ++k) {
+        e = hipEventCreateWithFlags(&ctx->slot[k].copied, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->slot[k].consumed, hipEventDisableTiming);
+    }
     delete h;
     if (e != hipSuccess) {
         std::string msg = std::string("fs_ctx_create: ") + hipGetErrorString(e);
@@ -130,13 +167,21 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
 fs_status fs_ctx_destroy(fs_ctx* ctx) {
     if (!ctx) return FS_E_INVALID;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+    if (ctx->compute_stream) (void)hipStreamSynchronize(ctx->compute_stream);
+    if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+    if (ctx->compute_stream) (void)hipStreamDestroy(ctx->compute_stream);
+    for (HostSlot& sl : ctx->slot) {
+        if (sl.copied) (void)hipEventDestroy(sl.copied);
+        if (sl.consumed) (void)hipEventDestroy(sl.consumed);
+        (void)hipFree(sl.d_frames);
+        (void)hipFree(sl.d_offsets);
+        (void)hipFree(sl.d_lengths);
+        (void)hipFree(sl.d_out);
+        (void)hipFree(sl.d_status);
+    }
+    if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     (void)hipFree(ctx->d_tables);
-    (void)hipFree(ctx->d_frames);
-    (void)hipFree(ctx->d_offsets);
-    (void)hipFree(ctx->d_lengths);
-    (void)hipFree(ctx->d_out);
-    (void)hipFree(ctx->d_status);
     delete ctx;
     return FS_SUCCESS;
 }
@@ -163,17 +208,70 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     if (!frames || !offsets || !lengths || !out)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: null pointer");
     FS_HIP(ctx, hipSetDevice(ctx->device));
-    fs_status st = ensure_staging(ctx, frames_bytes, n);
-    if (st != FS_SUCCESS) return st;
-    hipStream_t s = ctx->stream;
-    FS_HIP(ctx, hipMemcpyAsync(ctx->d_frames, frames, frames_bytes, hipMemcpyHostToDevice, s));
-    FS_HIP(ctx, hipMemcpyAsync(ctx->d_offsets, offsets, (size_t)n * 8, hipMemcpyHostToDevice, s));
-    FS_HIP(ctx, hipMemcpyAsync(ctx->d_lengths, lengths, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    FS_HIP(ctx, framesum::launch_digest(ctx->d_frames, ctx->d_offsets, ctx->d_lengths, n, mtu, ctx->d_tables,
-                                        ctx->d_out, status ? ctx->d_status : nullptr, s, ctx->num_cus));
-    FS_HIP(ctx, hipMemcpyAsync(out, ctx->d_out, (size_t)n * sizeof(fs_digest), hipMemcpyDeviceToHost, s));
-    if (status) FS_HIP(ctx, hipMemcpyAsync(status, ctx->d_status, n, hipMemcpyDeviceToHost, s));
-    FS_HIP(ctx, hipStreamSynchronize(s));
+    FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));  // the pinned mirrors are free
+    fs_status pst = ensure_pinned(ctx, n);
+    if (pst != FS_SUCCESS) return pst;
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pin);
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pin + (size_t)n * 8);
+    fs_digest* h_out = reinterpret_cast<fs_digest*>(ctx->h_pin + (size_t)n * 12);
+    uint8_t* h_st = ctx->h_pin + (size_t)n * 20;
+    std::memcpy(h_off, offsets, (size_t)n * 8);
+    std::memcpy(h_len, lengths, (size_t)n * 4);
+    uint32_t c0 = 0;
+    for (int chunk = 0; c0 < n; ++chunk) {
+        // frames [c0, c1): grow while the byte span [lo, hi) stays within kChunkBytes
+        uint64_t lo = offsets[c0], hi = offsets[c0] + lengths[c0];
+        uint32_t c1 = c0 + 1;
+        while (c1 < n && c1 - c0 < kChunkFrames) {
+            const uint64_t o = offsets[c1], e = o + lengths[c1];
+            const uint64_t nlo = o < lo ? o : lo, nhi = e > hi ? e : hi;
+            if (nhi - nlo > kChunkBytes) break;
+            lo = nlo;
+            hi = nhi;
+            ++c1;
+        }
+        if (c1 < n && c1 - c0 < 64 && hi - lo < kChunkBytes / 4) {
+            // the next frame lies far away (frames not stored in index order): one chunk
+            // spanning the rest of the batch instead of a launch per handful of frames
+            for (; c1 < n; ++c1) {
+                const uint64_t o = offsets[c1], e = o + lengths[c1];
+                lo = o < lo ? o : lo;
+                hi = e > hi ? e : hi;
+            }
+        }
+        for (uint32_t i = c0; i < c1; ++i)
+            if (offsets[i] + lengths[i] > frames_bytes)
+                return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(i) +
+                                                      " ends past frames_bytes");
+        // copy [cpy_lo, cpy_hi): 16-B aligned start with a 16-B prefix (sub-4-byte frames read
+        // up to 12 bytes before their start), end rounded up to the dword the engine may read
+        const uint64_t cpy_lo = (lo >= 16 ? lo - 16 : 0) & ~uint64_t(15);
+        uint64_t cpy_hi = (hi + 3) & ~uint64_t(3);
+        if (cpy_hi > frames_bytes) cpy_hi = frames_bytes;
+        HostSlot& sl = ctx->slot[chunk % kHostSlots];
+        const uint32_t cnt = c1 - c0;
+        fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, cnt);
+        if (st != FS_SUCCESS) return st;
+        hipStream_t cs = ctx->copy_stream, ks = ctx->compute_stream;
+        if (sl.used) FS_HIP(ctx, hipStreamWaitEvent(cs, sl.consumed, 0));  // chunk c - kHostSlots done with it
+        FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, cs));
+        FS_HIP(ctx, hipMemcpyAsync(sl.d_offsets, h_off + c0, (size_t)cnt * 8, hipMemcpyHostToDevice, cs));
+        FS_HIP(ctx, hipMemcpyAsync(sl.d_lengths, h_len + c0, (size_t)cnt * 4, hipMemcpyHostToDevice, cs));
+        FS_HIP(ctx, hipEventRecord(sl.copied, cs));
+        FS_HIP(ctx, hipStreamWaitEvent(ks, sl.copied, 0));
+        // the kernel addresses frame i at base + offsets[i]: base = staging - cpy_lo (4-B aligned)
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
+        FS_HIP(ctx, framesum::launch_digest(base, sl.d_offsets, sl.d_lengths, cnt, mtu, ctx->d_tables, sl.d_out,
+                                            status ? sl.d_status : nullptr, ks, ctx->num_cus));
+        FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
+        sl.used = true;
+        FS_HIP(ctx, hipMemcpyAsync(h_out + c0, sl.d_out, (size_t)cnt * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
+        if (status) FS_HIP(ctx, hipMemcpyAsync(h_st + c0, sl.d_status, cnt, hipMemcpyDeviceToHost, ks));
+        c0 = c1;
+    }
+    FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));
+    std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
+    if (status) std::memcpy(status, h_st, n);
     return FS_SUCCESS;
 }
 

@@ -22,12 +22,13 @@
 //     quad xor, then a final Z_(4-t) that also removes the t <= 3 zero bytes
 //     the dword rounding appended). Leading zero rows do not change a zero-init CRC; the CRC init
 //     is applied by XOR-ing the frame's first 4 bytes with 0xFF.
-//   * one's-complement sum: the same registers are summed as dwords (exact
-//     64-bit integer, so RecvEth's Sum16 fold is reproduced bit for bit incl.
-//     the 0x0000 / 0xFFFF edge) from frame dword 10 on (frame byte >= 37 > 34);
-//     the frame's lane adds/subtracts the exact native-domain contributions of
-//     the header/IP-option bytes, the Ethernet padding, the excluded words and
-//     the pseudo-header.
+//   * one's-complement sum: the same registers feed v_sad_u16 (acc += lo16 + hi16,
+//     one op per dword; congruent mod 65535 to the byte-swapped big-endian word
+//     sum) from frame dword 10 on (frame bytes >= 37, past byte 34); the group's lane 0 adds
+//     or subtracts, in the same domain, the header/IP-option bytes, the excluded
+//     words, the Ethernet padding and the pseudo-header, then folds with a
+//     positive offset so RecvEth's Sum16 result (incl. the 0x0000 / 0xFFFF edge)
+//     is reproduced bit for bit.
 //   * LDS tables: the hot Z64 (and Z4) tables are stored as 8 copies per table
 //     in a [entry][table*8+copy] layout, 256 B per entry. Lane L = c + 8h of a
 //     32-lane bank group reads table (k+h)&3 in its k-th lookup, so the 32
@@ -408,12 +409,13 @@ __device__ __forceinline__ void tile_descriptors(Tile& T, uint32_t tile, uint32_
                                                  const uint32_t* __restrict__ lengths, uint64_t& S) {
     T.fi = tile * kFramesPerTile + grp;
     T.fvalid = T.fi < n;
-    S = 0;
-    T.len = 0;
-    if (T.fvalid) {
-        S = offsets[T.fi];
-        T.len = lengths[T.fi];
-    }
+    // groups past the batch end borrow the last frame's offset with length 0, so their
+    // (masked) row loads stay next to real frame bytes (`frames` itself may lie outside
+    // the allocation: the host-staged path passes staging - first offset)
+    const uint32_t fl = T.fvalid ? T.fi : n - 1u;
+    S = offsets[fl];
+    T.len = lengths[fl];
+    if (!T.fvalid) T.len = 0;
 }
 
 // Wave max / min of a value that is uniform within each 4-lane group: two DPP row

@@ -130,9 +130,13 @@ class Engine:
         if st != FS_SUCCESS:
             raise FramesumError(f"fs_ctx_create({device}) failed ({st}): {self.lib.fs_last_error(None).decode()}")
         self._ctx = ctx
+        self._pinned: set[int] = set()
 
     def close(self) -> None:
         if getattr(self, "_ctx", None):
+            for addr in list(self._pinned):
+                self.lib.fs_host_free(self._ctx, ctypes.c_void_p(addr))
+            self._pinned.clear()
             self.lib.fs_ctx_destroy(self._ctx)
             self._ctx = None
 
@@ -183,14 +187,42 @@ class Engine:
         return out, status
 
     # ---- host-staged path (numpy in, numpy out) -----------------------------
-    def digest_host(self, frames: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, mtu: int = 0):
-        """Host buffers in, host results out (fs_digest_batch_host). Returns (digests, status)."""
+    def host_empty(self, shape, dtype=np.uint8) -> np.ndarray:
+        """A numpy array in pinned host memory (fs_host_alloc), freed with the array."""
+        import weakref
+
+        dtype = np.dtype(dtype)
+        nbytes = max(1, int(np.prod(shape)) * dtype.itemsize)
+        ptr = ctypes.c_void_p()
+        self._check(self.lib.fs_host_alloc(self._ctx, ctypes.c_uint64(nbytes), ctypes.byref(ptr)), "fs_host_alloc")
+        raw = (ctypes.c_uint8 * nbytes).from_address(ptr.value)
+        arr = np.frombuffer(raw, dtype=np.uint8, count=nbytes)[: int(np.prod(shape)) * dtype.itemsize]
+        arr = arr.view(dtype).reshape(shape)
+        # freed when the array goes away, or by close() (arrays must not outlive the engine)
+        self._pinned.add(ptr.value)
+        weakref.finalize(raw, Engine._free_pinned, weakref.ref(self), ptr.value)
+        return arr
+
+    @staticmethod
+    def _free_pinned(engine_ref, addr: int) -> None:
+        eng = engine_ref()
+        if eng is not None and getattr(eng, "_ctx", None) and addr in eng._pinned:
+            eng._pinned.discard(addr)
+            eng.lib.fs_host_free(eng._ctx, ctypes.c_void_p(addr))
+
+    def digest_host(self, frames: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, mtu: int = 0,
+                    out: Optional[np.ndarray] = None, status: Optional[np.ndarray] = None):
+        """Host buffers in, host results out (fs_digest_batch_host): chunked H2D / kernel / D2H
+        pipeline over the context's streams. Returns (digests, status)."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
         n = int(lengths.size)
-        out = np.zeros(n, dtype=DIGEST_DTYPE)
-        status = np.zeros(n, dtype=np.uint8)
+        if out is None:
+            out = np.zeros(n, dtype=DIGEST_DTYPE)
+        if status is None:
+            status = np.zeros(n, dtype=np.uint8)
+        assert out.dtype == DIGEST_DTYPE and out.size >= n and status.dtype == np.uint8 and status.size >= n
         if n == 0:
             return out, status
         st = self.lib.fs_digest_batch_host(

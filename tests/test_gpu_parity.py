@@ -177,3 +177,25 @@ def test_host_staged_path(engine):
 def test_empty_batch(engine):
     out, st = engine.digest_host(np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32))
     assert out.size == 0
+
+
+def test_host_staged_multichunk_unordered(engine):
+    # > 16 MiB of frames in shuffled buffer order: several pipeline chunks, non-monotonic
+    # offsets (chunk byte spans computed from min/max), pinned and pageable inputs
+    buf, off0, ln0 = synth.mixed_batch(12000, seed=9)
+    perm = np.random.default_rng(3).permutation(len(ln0))
+    for order in (np.arange(len(ln0)), perm):
+        off, ln = off0[order].astype(np.uint64), ln0[order].astype(np.uint32)
+        edig, est = coracle.digest_batch(buf, off.astype(np.int64), ln.astype(np.int32))
+        dig, st = engine.digest_host(buf, off, ln)
+        assert np.array_equal(dig, edig) and np.array_equal(st, est)
+    pin = engine.host_empty(buf.shape)
+    pin[:] = buf
+    dig2, st2 = engine.digest_host(pin, off, ln)
+    assert np.array_equal(dig2, edig) and np.array_equal(st2, est)
+
+
+def test_host_staged_rejects_out_of_range(engine):
+    buf = np.zeros(100, np.uint8)
+    with pytest.raises(Exception):
+        engine.digest_host(buf, np.array([90], np.uint64), np.array([20], np.uint32))
