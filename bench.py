@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
     p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather (N>1 diagnostics)")
+    p.add_argument("--streams", type=int, default=2,
+                   help="HIP streams the steps rotate over: step i+1's kernel starts on the CUs step i's "
+                        "tail frees (every batch is still fully digested)")
     return p.parse_args()
 
 
@@ -135,28 +138,40 @@ def main():
     bytes_per_batch = int(ln.astype(np.int64).sum())
     resident = sum(int(x[0].numel()) for x in batches)
     nb = len(batches)
-    outs = [torch.empty((n, 2), dtype=torch.int32, device=dev) for _ in range(2)]
-    stats = [torch.empty((n,), dtype=torch.uint8, device=dev) for _ in range(2)]
+    ns = max(1, args.streams)
+    nslot = max(2, ns)
+    outs = [torch.empty((n, 2), dtype=torch.int32, device=dev) for _ in range(nslot)]
+    stats = [torch.empty((n,), dtype=torch.uint8, device=dev) for _ in range(nslot)]
     gather = world > 1 and not args.no_gather
-    stream = torch.cuda.current_stream(dev)
+    main_stream = torch.cuda.current_stream(dev)
+    streams = [main_stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+    # a slot's previous gather / kernel must be finished before the slot is rewritten
+    slot_done = [None] * nslot
 
     pending = []
 
-    def step(i: int, ev=None):
+    def step(i: int, ev=None, stream=None):
         fb, fo, fl = batches[i % nb]
-        k = i & 1
-        if ev is not None:
-            ev[0].record(stream)
-        engine.digest_device(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
-        if gather:
-            # digests of step i go to rank 0 over RCCL while step i+1's kernel runs; the
-            # output slot is reused two steps later, so wait for that slot's gather first
-            while len(pending) >= 2:
-                pending.pop(0)()
-            _, finish = shard.gather_digests(outs[k], stats[k], world, rank, n * world, async_op=True)
-            pending.append(finish)
+        k = i % nslot
+        s = stream if stream is not None else streams[i % ns]
+        with torch.cuda.stream(s):
+            if slot_done[k] is not None:
+                s.wait_event(slot_done[k])
+            if ev is not None:
+                ev[0].record(s)
+            engine.digest_device(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=s)
+            if ev is not None:
+                ev[1].record(s)
+            if gather:
+                # digests of step i go to rank 0 over RCCL while later steps' kernels run;
+                # at most `nslot` gathers are pending (each slot is reused nslot steps later)
+                while len(pending) >= nslot:
+                    pending.pop(0)()
+                _, finish = shard.gather_digests(outs[k], stats[k], world, rank, n * world, async_op=True)
+                pending.append(finish)
+            done = torch.cuda.Event()
+            done.record(s)
+            slot_done[k] = done
 
     def drain():
         while pending:
@@ -189,7 +204,7 @@ def main():
     saved_gather = gather
     gather = False
     for i in range(args.steps):
-        step(i, kev[i])
+        step(i, kev[i], stream=main_stream)  # one stream: each event pair brackets one launch
     torch.cuda.synchronize()
     gather = saved_gather
     kms = sorted(a.elapsed_time(b) for a, b in kev)
@@ -228,6 +243,7 @@ def main():
                 "global_batch_frames": n * world,
                 "parallelism": f"frames sharded round-robin over {world} GPU(s); RCCL gather of digests to rank 0"
                 if world > 1 else "single GPU",
+                "streams": ns,
             },
             "roofline": {
                 "bound": "hbm",

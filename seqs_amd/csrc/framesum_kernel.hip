@@ -53,6 +53,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_DMA_FIRST
 #define FS_DMA_FIRST 1  // 1: table LDS-DMA before the descriptors (ahead of the first rows)
 #endif
+#ifndef FS_NT
+#define FS_NT 0  // 1: non-temporal row loads
+#endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio in the row loop (see stream_rows)
 #endif
@@ -168,7 +171,9 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xffu) <<
 // the frame are clamped to `lo` (the frame's first chunk, never below the buffer
 // start) and realigned / masked by the slow path. Rows never run past the frame's last dword (see the segments).
 __device__ __forceinline__ u32x4 load_chunk(const uint32_t* fb, int rel, int lo) {
-    return *reinterpret_cast<const u32x4_a4*>(fb + max(rel, lo));
+    const u32x4_a4* p = reinterpret_cast<const u32x4_a4*>(fb + max(rel, lo));
+    if (FS_NT) return __builtin_nontemporal_load(p);  // streamed once: no reuse in L2
+    return *p;
 }
 
 // One's-complement accumulation: v_sad_u16(x, 0, acc) = acc + x[15:0] + x[31:16] in ONE op.

@@ -13,12 +13,19 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
+template <bool NT>
+__device__ __forceinline__ u32x4 ld4(const u32x4* p) {
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+template <bool NT>
 __global__ void k_stream(const u32x4* __restrict__ p, size_t n16, uint32_t* out) {
     uint32_t acc = 0;
     size_t stride = (size_t)gridDim.x * blockDim.x;
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (; i + 3 * stride < n16; i += 4 * stride) {
-        u32x4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+        u32x4 a = ld4<NT>(p + i), b = ld4<NT>(p + i + stride), c = ld4<NT>(p + i + 2 * stride), d = ld4<NT>(p + i + 3 * stride);
         acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
     }
     for (; i < n16; i += stride) { u32x4 a = p[i]; acc ^= a.x ^ a.y ^ a.z ^ a.w; }
@@ -26,7 +33,7 @@ __global__ void k_stream(const u32x4* __restrict__ p, size_t n16, uint32_t* out)
 }
 
 // G lanes per frame (64/G frames per wave), rows of G*16 bytes anchored at the frame end.
-template <int kPF, int G>
+template <int kPF, int G, bool NT = false>
 __global__ void __launch_bounds__(1024) k_frames(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
                                                  uint32_t* out) {
     constexpr int FPW = 64 / G, RD = 4 * G;  // frames per wave, row dwords
@@ -48,13 +55,14 @@ __global__ void __launch_bounds__(1024) k_frames(const uint8_t* __restrict__ bas
         const int lo = -(int)min(sdw, (uint64_t)(1 << 24));
         u32x4 pf[kPF];
 #pragma unroll
-        for (int i = 0; i < kPF; ++i) pf[i] = *reinterpret_cast<const u32x4_a4*>(fb + max(rel0 + RD * i, lo));
+        for (int i = 0; i < kPF; ++i) pf[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4*>(fb + max(rel0 + RD * i, lo))) : *reinterpret_cast<const u32x4_a4*>(fb + max(rel0 + RD * i, lo));
         for (int r0 = 0; r0 < Rp; r0 += kPF) {
 #pragma unroll
             for (int i = 0; i < kPF; ++i) {
                 const int rel = rel0 + RD * (r0 + i);
                 acc = (acc * 3) ^ pf[i].x ^ pf[i].y ^ pf[i].z ^ pf[i].w;
-                pf[i] = *reinterpret_cast<const u32x4_a4*>(fb + max(min(rel + RD * kPF, rel_last), lo));
+                const u32x4_a4* q = reinterpret_cast<const u32x4_a4*>(fb + max(min(rel + RD * kPF, rel_last), lo));
+                pf[i] = NT ? __builtin_nontemporal_load(q) : *q;
             }
         }
     }
@@ -62,8 +70,9 @@ __global__ void __launch_bounds__(1024) k_frames(const uint8_t* __restrict__ bas
 }
 
 int main(int argc, char** argv) {
-    const size_t nbytes = 98304000;
-    const int NB = 4, iters = 100;
+    const size_t nbytes = argc > 1 ? (size_t)atoll(argv[1]) : 98304000;
+    const int NB = (int)((1200000000ull + nbytes - 1) / nbytes) < 4 ? 4 : (int)((1200000000ull + nbytes - 1) / nbytes);
+    const int iters = 50;
     std::vector<uint8_t*> bufs(NB);
     for (auto& b : bufs) {
         CHECK(hipMalloc(&b, nbytes + 4096));
@@ -77,6 +86,7 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
+    printf("buffer %zu bytes, %d rotated\n", nbytes, NB);
     auto timeit = [&](auto launch, const char* name) {
         for (int i = 0; i < 10; ++i) launch(i);
         CHECK(hipDeviceSynchronize());
@@ -89,28 +99,22 @@ int main(int argc, char** argv) {
         double us = ms * 1e3 / iters;
         printf("%-44s %9.2f us/launch  %8.1f GB/s\n", name, us, nbytes / (us * 1e-6) / 1e9);
     };
-    for (int mult : {1, 2, 4, 8}) {
+    for (int mult : {2, 4, 8}) {
         char nm[128];
         snprintf(nm, sizeof nm, "stream dwordx4 grid=%dx%d", cus * mult, 256);
-        timeit([&](int i) { hipLaunchKernelGGL(k_stream, dim3(cus * mult), dim3(256), 0, 0,
+        timeit([&](int i) { hipLaunchKernelGGL(k_stream<false>, dim3(cus * mult), dim3(256), 0, 0,
+                                               (const u32x4*)bufs[i % NB], nbytes / 16, out); }, nm);
+        snprintf(nm, sizeof nm, "stream dwordx4 nt grid=%dx%d", cus * mult, 256);
+        timeit([&](int i) { hipLaunchKernelGGL(k_stream<true>, dim3(cus * mult), dim3(256), 0, 0,
                                                (const u32x4*)bufs[i % NB], nbytes / 16, out); }, nm);
     }
-    for (int mult : {4, 8}) {
-        char nm[128];
-        snprintf(nm, sizeof nm, "stream dwordx4 +4B misaligned grid=%dx256", cus * mult);
-        timeit([&](int i) { hipLaunchKernelGGL(k_stream, dim3(cus * mult), dim3(256), 0, 0,
-                                               (const u32x4*)(bufs[i % NB] + 4), nbytes / 16 - 1, out); }, nm);
-    }
-    const uint32_t nf = 65536, fl = 1500;
-#define FR(PF, G, GRID, NAME) timeit([&](int i) { hipLaunchKernelGGL((k_frames<PF, G>), dim3(GRID), dim3(1024), 0, 0, bufs[i % NB], nf, fl, out); }, NAME)
-    FR(4, 4, cus, "frames G=4  PF=4 (current kernel pattern)");
-    FR(2, 4, cus, "frames G=4  PF=2");
-    FR(6, 4, cus, "frames G=4  PF=6");
-    FR(4, 16, cus, "frames G=16 PF=4");
-    FR(2, 16, cus, "frames G=16 PF=2");
-    FR(2, 64, cus, "frames G=64 PF=2");
-    FR(1, 64, cus, "frames G=64 PF=1");
-    FR(4, 4, cus / 2, "frames G=4  PF=4 half grid (8 waves/CU eq)");
-    FR(8, 4, cus / 2, "frames G=4  PF=8 half grid");
+    const uint32_t fl = 1500, nf = (uint32_t)(nbytes / fl);
+#define FR(PF, G, NT, GRID, NAME) timeit([&](int i) { hipLaunchKernelGGL((k_frames<PF, G, NT>), dim3(GRID), dim3(1024), 0, 0, bufs[i % NB], nf, fl, out); }, NAME)
+    FR(6, 4, false, cus, "frames G=4  PF=6");
+    FR(6, 4, true, cus, "frames G=4  PF=6 nt");
+    FR(4, 16, false, cus, "frames G=16 PF=4");
+    FR(4, 16, true, cus, "frames G=16 PF=4 nt");
+    FR(2, 64, false, cus, "frames G=64 PF=2");
+    FR(2, 64, true, cus, "frames G=64 PF=2 nt");
     return 0;
 }
