@@ -12,8 +12,9 @@
 //     the head row is the partial one; lane l of the group loads dwords
 //     [4l, 4l+4) of every row with one global_load_dwordx4 (16 B/lane), kPrefetch
 //     rows ahead. The row loop depends only on the frame descriptor (offset,
-//     length); the header parse runs inside it (once the header rows have been
-//     captured into LDS), hidden behind the rows in flight.
+//     length); the frame's first 128 bytes are fetched into LDS by LDS-DMA next to
+//     the first rows, and the header parse runs after the first block of rows,
+//     hidden behind the rows in flight.
 //   * CRC: each lane keeps 4 independent dword STREAMS; a stream's successive
 //     dwords are 64 B apart, so its Horner step is  A <- Z64(A) ^ w  with Z64 a
 //     fixed GF(2) linear map evaluated by 4 byte-table lookups in LDS. After the
@@ -24,9 +25,9 @@
 //     is applied by XOR-ing the frame's first 4 bytes with 0xFF.
 //   * one's-complement sum: the same registers feed v_sad_u16 (acc += lo16 + hi16,
 //     one op per dword; congruent mod 65535 to the byte-swapped big-endian word
-//     sum) from frame dword 10 on (frame bytes >= 37, past byte 34); the group's lane 0 adds
-//     or subtracts, in the same domain, the header/IP-option bytes, the excluded
-//     words, the Ethernet padding and the pseudo-header, then folds with a
+//     sum) over every frame byte; the group's lane 0 subtracts, in the same
+//     domain, the Ethernet + IP header bytes, the excluded words and the Ethernet
+//     padding and adds the pseudo-header, then folds with a
 //     positive offset so RecvEth's Sum16 result (incl. the 0x0000 / 0xFFFF edge)
 //     is reproduced bit for bit.
 //   * LDS tables: the hot Z64 (and Z4) tables are stored as 8 copies per table
@@ -69,13 +70,16 @@ constexpr int kThreads = kWave * kWavesPerBlock;
 constexpr int kFramesPerTile = 16;
 constexpr int kRowDwords = 16;
 constexpr int kPrefetch = FS_PREFETCH;
-constexpr int kHdrDwords = 28;              // frame bytes [0, 112) staged for the header parse
-// + a 16-B guard for chunks that start before the frame, + 8 B so consecutive slots are 34 dwords
-// apart: the 16 frame lanes reading dword k of their slots hit 16 distinct banks (ds_read_b32
-// banks are (a/4) mod 32; a 32-dword stride made every parse read a 16-way conflict)
-constexpr int kHdrSlotBytes = 16 + 4 * kHdrDwords + 8;
+// Header slots: the row loop writes every loaded 16-B chunk that holds frame dwords [0, 28)
+// into the group's slot, at the dwords it was loaded from (a clamped head chunk lands at the
+// frame start; its bytes before the frame go to the slot's 16-B guard). Slots are 36 dwords
+// apart, so the 8 parser lanes of a 32-lane bank group read distinct banks.
+constexpr int kHdrDwords = 28;
+constexpr uint32_t kHdrSlotBytes = 144;
+static_assert(kHdrSlotBytes >= 16 + 4 * (kHdrDwords + 3) + 4, "slot holds the guard + the last chunk");
+constexpr uint32_t kHdrWaveBytes = kHdrSlotBytes * kFramesPerTile;
 constexpr int kStashBytes = 68;             // the frame's last row (Ethernet padding source); 17-dword stride
-constexpr int kCsumRel0 = 10;               // streamed checksum starts at frame dword 10
+constexpr int kFastRel0 = 2;                // rows whose chunks start at dword >= 2 carry no head/init mask
 
 // LDS map (bytes). [0, 88 KB) is FsTables verbatim (filled by LDS-DMA).
 constexpr uint32_t kLdsZ32 = 65536;
@@ -86,7 +90,7 @@ constexpr uint32_t kLdsZ12 = kLdsZ48 + 4096;
 constexpr uint32_t kLdsZ8 = kLdsZ12 + 4096;
 constexpr uint32_t kLdsTables = kLdsZ8 + 4096;
 constexpr uint32_t kLdsHdr = kLdsTables;
-constexpr uint32_t kLdsStash = kLdsHdr + kWavesPerBlock * kFramesPerTile * kHdrSlotBytes;
+constexpr uint32_t kLdsStash = kLdsHdr + kWavesPerBlock * kHdrWaveBytes;
 constexpr uint32_t kLdsBytes = kLdsStash + kWavesPerBlock * kFramesPerTile * kStashBytes;
 static_assert(kLdsHdr % 16 == 0 && kLdsStash % 16 == 0, "slots must be 16-B aligned");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
@@ -185,8 +189,9 @@ __device__ __forceinline__ uint32_t sad16(uint32_t x, uint32_t acc) { return __b
 // Per-frame row parameters, held by every lane of the frame's group.
 struct RowMasks {
     int nd;              // frame dwords (incl. the partial last one); 0 = nothing to stream
-    int fast_lo, fast_hi;
-    uint32_t head_mask, init0, init1, tail_mask;
+    uint32_t head_mask;  // bytes of dword 0 inside the frame; also the CRC init's part in dword 0
+    uint32_t init1;      // the CRC init's part in dword 1
+    uint32_t tail_mask;  // bytes of dword nd-1 inside the frame
 };
 
 __device__ __forceinline__ void process_row(char* lds, const LaneKeys& keys, u32x4 v, int rel, bool fast,
@@ -219,37 +224,30 @@ __device__ __forceinline__ void process_row(char* lds, const LaneKeys& keys, u32
             const int rj = rel + j;
             uint32_t d = (rj >= 0) ? v[j] : 0u;
             uint32_t x = 0u;
-            if (rj == 0) { d &= m.head_mask; x = m.init0; }
+            if (rj == 0) { d &= m.head_mask; x = m.head_mask; }
             if (rj == 1) x = m.init1;
             if (rj == m.nd - 1) d &= m.tail_mask;
             A[j] = zrep(lds, A[j], keys, 0, d ^ x);
-            cs = sad16((rj >= kCsumRel0) ? d : 0u, cs);
+            cs = sad16(d, cs);
         }
     }
 }
 
-// The frame's first 112 bytes go to the group's header slot (chunks starting before the
-// frame spill their garbage part into the slot's 16-B guard). Only the leading rows call it.
-__device__ __forceinline__ void capture_header(char* lds, uint32_t hdr_slot, int rel, int lo, u32x4 v) {
-    if (rel > -4 && rel < kHdrDwords) {
-        const int sh = max(rel, lo) - rel;
-        if (sh > 0 && sh < 4) {  // clamped load: realign as process_row does
-            const u32x4 u = v;
-            v.w = (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
-            v.z = (sh == 1) ? u.y : (sh == 2) ? u.x : 0u;
-            v.y = (sh == 1) ? u.x : 0u;
-            v.x = 0u;
-        }
-        *reinterpret_cast<u32x4*>(lds + hdr_slot + 16u + 4u * (uint32_t)rel) = v;
-    }
+// ---- parser-lane helpers over the LDS header slot (absolute-dword aligned: slot
+// dword k = the frame's dword k counted from its first dword, frame byte p at slot byte
+// 16 + sa + p). `hb` = the group's slot.
+__device__ __forceinline__ uint32_t hdr_dw(const char* lds, uint32_t hb, uint32_t k) {
+    return lds32(lds, hb + 16u + 4u * k);
 }
 
-// ---- frame-lane helpers over the LDS header slot (absolute-dword aligned: slot
-// dword k = frame-relative dword k, frame byte p at slot byte sa + p).
-__device__ __forceinline__ uint32_t slot_dw(const char* lds, uint32_t slot, uint32_t k) { return lds32(lds, slot + 16u + 4u * k); }
+// Row data -> header slot: the chunk's 16 bytes are frame dwords [p, p+4), p = max(rel, lo).
+__device__ __forceinline__ void capture_header(char* lds, uint32_t hb, int rel, int lo, u32x4 v) {
+    const int p = max(rel, lo);
+    if (p < kHdrDwords) *reinterpret_cast<u32x4*>(lds + hb + 16u + 4u * (uint32_t)p) = v;
+}
 // frame bytes [4j, 4j+4) as a little-endian dword
-__device__ __forceinline__ uint32_t frame_dw(const char* lds, uint32_t slot, uint32_t sa, uint32_t j) {
-    return __builtin_amdgcn_alignbyte(slot_dw(lds, slot, j + 1), slot_dw(lds, slot, j), sa);
+__device__ __forceinline__ uint32_t frame_dw(const char* lds, uint32_t hb, uint32_t sa, uint32_t j) {
+    return __builtin_amdgcn_alignbyte(hdr_dw(lds, hb, j + 1), hdr_dw(lds, hb, j), sa);
 }
 // bytes of absolute dword k that lie in the absolute byte range [a0, a1)
 __device__ __forceinline__ uint32_t range_mask(int k, int a0, int a1) {
@@ -258,9 +256,9 @@ __device__ __forceinline__ uint32_t range_mask(int k, int a0, int a1) {
     const uint32_t mlo = (lo >= 4) ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
     return mhi & ~mlo;
 }
-// sum, in the accumulator's 16-bit-half domain, of frame bytes [p0, p1) taken from a
-// dword-aligned LDS image whose dword 0 is frame-relative dword `d0` at byte `base`
-// (slot: base = slot + 16, d0 = 0; stash: d0 = nd - 16). Bytes outside the image count 0.
+// sum, in the accumulator's 16-bit-half domain, of frame bytes [p0, p1) taken from the
+// contiguous stash image whose dword 0 is the frame's dword `d0` (= nd - 16). Bytes outside
+// the image count 0.
 __device__ uint32_t nsum_lds(const char* lds, uint32_t base, int d0, int ndw, uint32_t sa, int p0, int p1) {
     uint32_t s = 0;
     if (p1 <= p0) return s;
@@ -269,6 +267,14 @@ __device__ uint32_t nsum_lds(const char* lds, uint32_t base, int d0, int ndw, ui
         const int i = k - d0;
         if (i >= 0 && i < ndw) s = sad16(lds32(lds, base + 4u * (uint32_t)i) & range_mask(k, a0, a1), s);
     }
+    return s;
+}
+// the same over the header image (frame bytes [p0, p1) with p1 <= 4 * kHdrDwords - sa)
+__device__ uint32_t nsum_hdr(const char* lds, uint32_t hb, uint32_t sa, int p0, int p1) {
+    uint32_t s = 0;
+    if (p1 <= p0) return s;
+    const int a0 = (int)sa + p0, a1 = (int)sa + p1;
+    for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s = sad16(hdr_dw(lds, hb, (uint32_t)k) & range_mask(k, a0, a1), s);
     return s;
 }
 
@@ -286,14 +292,14 @@ struct Parsed {
 
 // Header parse for one frame (frame lane). Gates follow stacks/portstack.go:163-308
 // exactly (oracle/framesum_oracle.c restates them line by line; the parity tests
-// compare the two). Reads only the LDS header slot.
-__device__ Parsed parse_frame(const char* lds, uint32_t slot, uint32_t sa, uint32_t len, uint32_t mtu) {
+// compare the two). Reads only the LDS header image.
+__device__ Parsed parse_frame(const char* lds, uint32_t hb, uint32_t sa, uint32_t len, uint32_t mtu) {
     Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0};
     if (len < 34u) { r.verdict = V_SMOL; return r; }                          // portstack.go:167-168
     if (mtu != 0 && len > mtu) { r.verdict = V_MTU; return r; }              // :169-172
     uint32_t bs[9];                                                           // bswap32(frame dword j), j = 3..8
 #pragma unroll
-    for (uint32_t j = 3; j < 9; ++j) bs[j] = __builtin_bswap32(frame_dw(lds, slot, sa, j));
+    for (uint32_t j = 3; j < 9; ++j) bs[j] = __builtin_bswap32(frame_dw(lds, hb, sa, j));
     const uint32_t etype = bs[3] >> 16;                                       // headers.go:209-215
     const uint32_t vihl = (bs[3] >> 8) & 0xffu;
     {   // eth/headers.go:333-340 via Put (:289-301): version forced to 4, checksum zeroed, 20 bytes.
@@ -320,7 +326,7 @@ __device__ Parsed parse_frame(const char* lds, uint32_t slot, uint32_t sa, uint3
     const uint32_t q = (off - 2u) >> 2;
     uint32_t lb[6];
 #pragma unroll
-    for (uint32_t i = 0; i < 6; ++i) lb[i] = __builtin_bswap32(frame_dw(lds, slot, sa, q + i));
+    for (uint32_t i = 0; i < 6; ++i) lb[i] = __builtin_bswap32(frame_dw(lds, hb, sa, q + i));
     const uint32_t sport = lb[0] & 0xffffu, dport = lb[1] >> 16;
     uint32_t lenword, excl;
     if (proto == 17u) {                                                       // :222-244
@@ -346,21 +352,49 @@ __device__ Parsed parse_frame(const char* lds, uint32_t slot, uint32_t sa, uint3
     r.compute = 1;
     r.off = off;
     r.end = end;
-    // Total over [off, end) = streamed frame bytes >= P10 + these corrections (+ the padding
-    // correction applied at the end, from the stash), all in the 16-bit-half domain.
-    const int P10 = 4 * kCsumRel0 - (int)sa;  // first streamed frame byte
+    // Total over [off, end) = all streamed frame bytes [0, len) + these corrections (+ the
+    // padding correction applied at the end, from the stash), all in the 16-bit-half domain.
     int64_t t = 0;
-    t -= (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, (int)(off + excl),
-                           (int)(off + excl + (proto == 6u ? 4u : 2u)));
+    t -= (int64_t)nsum_hdr(lds, hb, sa, (int)(off + excl), (int)(off + excl + (proto == 6u ? 4u : 2u)));
     r.parity = (int)((sa + off) & 1u);
     const uint32_t w[6] = {bs[6] & 0xffffu, bs[7] >> 16, bs[7] & 0xffffu, bs[8] >> 16, proto, lenword};
 #pragma unroll
     for (int i = 0; i < 6; ++i) t += (int64_t)(r.parity ? w[i] : bswap16(w[i]));
     r.corr_fixed = t;
-    if ((int)off < P10) t += (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, (int)off, P10);
-    else t -= (int64_t)nsum_lds(lds, slot + 16u, 0, kHdrDwords, sa, P10, (int)off);
+    t -= (int64_t)nsum_hdr(lds, hb, sa, 0, (int)off);  // the Ethernet + IP header bytes
     r.corr = t;
     return r;
+}
+
+// The parse result lives in LDS while the rows stream (it would otherwise hold 11 VGPRs
+// across the row loops): dwords 0..13 of the group's header slot, dead after the parse and
+// rewritten only by the next tile's rows, after this tile's finish.
+// The frame's descriptor (offset, length) is parked next to it (dwords 11..13).
+__device__ __forceinline__ void park_parsed(char* lds, uint32_t hb, const Parsed& P, uint64_t S, uint32_t len) {
+    const uint32_t v[14] = {P.verdict, P.ip_csum, P.stored, (uint32_t)P.compute, (uint32_t)P.parity, P.off, P.end,
+                            (uint32_t)P.corr, (uint32_t)((uint64_t)P.corr >> 32), (uint32_t)P.corr_fixed,
+                            (uint32_t)((uint64_t)P.corr_fixed >> 32), (uint32_t)S, (uint32_t)(S >> 32), len};
+#pragma unroll
+    for (uint32_t k = 0; k < 14; ++k)
+        *reinterpret_cast<uint32_t*>(lds + hb + 16u + 4u * k) = v[k];
+}
+__device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hb, uint64_t& S, uint32_t& len) {
+    uint32_t v[14];
+#pragma unroll
+    for (uint32_t k = 0; k < 14; ++k) v[k] = hdr_dw(lds, hb, k);
+    S = ((uint64_t)v[12] << 32) | v[11];
+    len = v[13];
+    Parsed P;
+    P.verdict = v[0];
+    P.ip_csum = v[1];
+    P.stored = v[2];
+    P.compute = (int)v[3];
+    P.parity = (int)v[4];
+    P.off = v[5];
+    P.end = v[6];
+    P.corr = (int64_t)(((uint64_t)v[8] << 32) | v[7]);
+    P.corr_fixed = (int64_t)(((uint64_t)v[10] << 32) | v[9]);
+    return P;
 }
 
 // Final L4 checksum + verdict (frame lane) once the streamed sum is known.
@@ -402,9 +436,15 @@ __device__ uint32_t finish_l4(const char* lds, uint32_t stash, const uint32_t* f
 // so no lane-to-lane broadcast is needed anywhere on the tile's critical path.
 struct Tile {
     bool fvalid;
-    uint32_t fi, len, nd, sa, te;
+    uint32_t fi, len, nd, ndall, sa, te;
     uint64_t E, sdw;
-    int R, Rp, Rsplit, rel0, lo;
+    // row/header load addressing: the group's own frame, or for an empty group (no frame, or
+    // a frame under 4 bytes, whose streams are never used) a longest frame of the tile, so
+    // that every load -- including the unclamped fast-path refills -- stays inside a frame
+    uint64_t ld_sdw;
+    int ld_nd, ld_ndall;
+    int R, Rp, rel0, lo;
+    int Rh;            // wave-uniform: last row holding header dwords [0, kHdrDwords) of any frame
     int RF_lo, RF_hi;  // wave-uniform rows where every lane takes the fast path
     const uint32_t* gfb;
 };
@@ -414,9 +454,9 @@ __device__ __forceinline__ void tile_descriptors(Tile& T, uint32_t tile, uint32_
                                                  const uint32_t* __restrict__ lengths, uint64_t& S) {
     T.fi = tile * kFramesPerTile + grp;
     T.fvalid = T.fi < n;
-    // groups past the batch end borrow the last frame's offset with length 0, so their
-    // (masked) row loads stay next to real frame bytes (`frames` itself may lie outside
-    // the allocation: the host-staged path passes staging - first offset)
+    // groups past the batch end read the last frame's descriptor with length 0 (their loads
+    // then use a longest frame of the tile, see tile_geometry; `frames` itself may lie
+    // outside the allocation: the host-staged path passes staging - first offset)
     const uint32_t fl = T.fvalid ? T.fi : n - 1u;
     S = offsets[fl];
     T.len = lengths[fl];
@@ -439,32 +479,41 @@ __device__ __forceinline__ int group_reduce(int x) {
 __device__ __forceinline__ void tile_geometry(Tile& T, uint64_t S, uint32_t gl, const uint8_t* __restrict__ frames) {
     T.E = S + T.len;
     T.sdw = S >> 2;
-    const uint32_t ndall = (uint32_t)(((T.E + 3u) >> 2) - T.sdw);
-    T.nd = (T.fvalid && T.len >= 4u) ? ndall : 0u;
+    T.ndall = (uint32_t)(((T.E + 3u) >> 2) - T.sdw);
+    T.nd = (T.fvalid && T.len >= 4u) ? T.ndall : 0u;
     T.sa = (uint32_t)(S & 3u);
     T.te = (uint32_t)(T.E & 3u) ? (uint32_t)(T.E & 3u) : 4u;
-    T.gfb = reinterpret_cast<const uint32_t*>(frames + (T.sdw << 2));
     const int nd = (int)T.nd;
-    T.R = group_reduce<true>((nd + kRowDwords - 1) / kRowDwords);
+    const int rows = (nd + kRowDwords - 1) / kRowDwords;
+    T.R = group_reduce<true>(rows);
+    {
+        const uint64_t ball = __ballot(rows == T.R);  // never 0: some lane holds the maximum
+        const int src = (int)__builtin_ctzll(ball);
+        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)T.sdw, src);
+        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(T.sdw >> 32), src);
+        const int s_nd = __builtin_amdgcn_readlane(nd, src);
+        const bool borrow = nd == 0;
+        T.ld_sdw = borrow ? (((uint64_t)s_hi << 32) | s_lo) : T.sdw;
+        T.ld_nd = borrow ? s_nd : nd;
+        T.ld_ndall = borrow ? s_nd : (int)T.ndall;
+    }
     // Rows padded at the FRONT to a multiple of kPrefetch: leading all-zero rows
     // leave a zero-init CRC stream unchanged, so the loop needs no tail guard.
     T.Rp = (T.R + kPrefetch - 1) / kPrefetch * kPrefetch;
+    T.gfb = reinterpret_cast<const uint32_t*>(frames + (T.ld_sdw << 2));
     const int base0 = nd - kRowDwords * T.Rp;  // rel of the group's lane 0 in row 0
-    T.rel0 = base0 + 4 * (int)gl;
-    // Rsplit: first row (multiple of kPrefetch) by which every frame's header dwords
-    // [0, 28) have streamed through the slot; the header parse runs there.
-    const int rh = group_reduce<true>(nd > 0 ? (min(kHdrDwords - 1, nd - 1) - base0) / kRowDwords : -1);
-    T.Rsplit = min(T.Rp, (rh + kPrefetch) / kPrefetch * kPrefetch);
+    T.rel0 = T.ld_nd - kRowDwords * T.Rp + 4 * (int)gl;
+    T.Rh = group_reduce<true>(nd > 0 ? (kHdrDwords - 1 - base0) / kRowDwords : -1);
     // Loads of rows that start before the frame are clamped to the frame's first chunk (its last
     // chunk for frames under 4 dwords), so lanes idling through a tile's longest frame re-read
     // one cached line instead of fetching the bytes that precede their frame; never below frames[0].
-    T.lo = max(T.sdw > (1u << 24) ? -(1 << 24) : -(int)T.sdw, min(0, nd - 4));
-    // Fast rows: every lane's chunk [rel, rel+4) inside [kCsumRel0, nd - 1) (no head/tail/init
+    T.lo = max(T.ld_sdw > (1u << 24) ? -(1 << 24) : -(int)T.ld_sdw, min(0, T.ld_nd - 4));
+    // Fast rows: every lane's chunk [rel, rel+4) inside [kFastRel0, nd - 1) (no head/tail/init
     // masks, whole chunk streamed into the checksum): lane 0 of the group bounds the start,
     // lane 3 the end. Empty groups stream zeros and never force the slow path.
     int flo = -0x40000000, fhi = 0x40000000;
     if (nd > 0) {
-        const int a = kCsumRel0 - base0, b = nd - 5 - (base0 + 12);  // rows r with a <= 16 r <= b
+        const int a = kFastRel0 - base0, b = nd - 5 - (base0 + 12);  // rows r with a <= 16 r <= b
         flo = (a <= 0) ? 0 : (a + kRowDwords - 1) / kRowDwords;
         fhi = (b < 0) ? -1 : b / kRowDwords;
     }
@@ -497,10 +546,10 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     const uint32_t gwave = blockIdx.x * kWavesPerBlock + wave;
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
     const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
-    const uint32_t hdr_base = kLdsHdr + wave * (kFramesPerTile * kHdrSlotBytes);
+    const uint32_t hdr_wave = kLdsHdr + wave * kHdrWaveBytes;
     const uint32_t stash_base = kLdsStash + wave * (kFramesPerTile * kStashBytes);
 
-    const uint32_t gslot = hdr_base + grp * kHdrSlotBytes;      // the group's header slot
+    const uint32_t hb = hdr_wave + kHdrSlotBytes * grp;         // the group's header slot
     const uint32_t stash = stash_base + grp * kStashBytes;      // the group's last-row stash
     LaneKeys keys;
     {
@@ -535,17 +584,23 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     __builtin_amdgcn_s_waitcnt(0x0f70);  // fine-stamp build only: time the descriptor round trip
     FS_STAMP(8);
 #endif
+    bool rows0 = false;  // the first tile has rows (and so a row prefetch in flight)
     if (__builtin_amdgcn_readfirstlane(tile) < ntiles) {
         tile_geometry(T, S, gl, frames);
+        rows0 = T.Rp > 0;
+        if (rows0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-        for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
+            for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
+        }
     }
     FS_STAMP(9);
 #if !FS_DMA_FIRST
     table_dma(tabs, lds, wave, lane);
 #endif
 #if FS_DMA_FIRST
-    __builtin_amdgcn_s_waitcnt(0x0f70 | kPrefetch);  // vmcnt(kPrefetch): the table pieces are older
+    // the table pieces are older than the rows
+    if (rows0) __builtin_amdgcn_s_waitcnt(0x0f70 | kPrefetch);
+    else __builtin_amdgcn_s_waitcnt(0x0f70);
 #else
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): table pieces and the first rows
 #endif
@@ -556,65 +611,93 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     while (tile < ntiles) {
         RowMasks M;
         M.nd = (int)T.nd;
-        if (T.nd > 0) {
-            M.fast_lo = kCsumRel0;
-            M.fast_hi = (int)T.nd - 5;
-        } else {  // empty group: every row streams zeros
-            M.fast_lo = -0x40000000;
-            M.fast_hi = 0x40000000;
-        }
         M.head_mask = 0xffffffffu << (8u * T.sa);
-        M.init0 = M.head_mask;
         M.init1 = (1u << (8u * T.sa)) - 1u;
         M.tail_mask = (T.te == 4u) ? 0xffffffffu : ((1u << (8u * T.te)) - 1u);
 
-        // ---- main loop: rows 0..Rp-1 with kPrefetch rows in flight, in three segments:
-        //   A [0, min(Rsplit, Rc))  capture the header rows into LDS, refill
-        //   B [.., Rc)              refill only
-        //   C [Rc, Rp)              the last kPrefetch rows: no refill (nothing past the frame end)
-        // The header parse runs between A and B (or after C when the header rows reach C),
-        // while the ring's loads are in flight.
+        // ---- main loop: rows 0..Rp-1 in blocks of kPrefetch rows with kPrefetch rows in
+        // flight; the last block does not refill (nothing lies past the frame end). Blocks
+        // whose rows are all fast for every lane run the lean path: four Z64 steps + four
+        // v_sad_u16 per row and a refill with an immediate row offset.
         uint32_t A[4] = {0u, 0u, 0u, 0u};
         uint32_t cs = 0u;
-        auto stream_rows = [&](int rbeg, int rend, auto hdr_tag, auto refill_tag) {
-            constexpr bool kHdr = decltype(hdr_tag)::value, kRefill = decltype(refill_tag)::value;
-            for (int r0 = rbeg; r0 < rend; r0 += kPrefetch) {
-                // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
-                // a wave with more rows left gets a higher priority.
-                if (FS_PRIO) {
-                    const int left4 = (4 * (T.Rp - r0)) / max(T.Rp, 1);  // 4 .. 1
-                    if (left4 >= 4) __builtin_amdgcn_s_setprio(3);
-                    else if (left4 == 3) __builtin_amdgcn_s_setprio(2);
-                    else if (left4 == 2) __builtin_amdgcn_s_setprio(1);
-                    else __builtin_amdgcn_s_setprio(0);
-                }
+        const bool parser = T.fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
+        // the header parse runs once the block holding row Rh (the last row with header dwords)
+        // has been captured, while the ring's loads are in flight
+        const uint64_t fS = T.E - T.len;
+        const uint32_t fsa = T.sa, flen = T.len;
+        auto parse = [&]() {
+            if (parser) park_parsed(lds, hb, parse_frame(lds, hb, fsa, flen, mtu), fS, flen);
+        };
+        auto prio = [&](int r0) {
+            // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
+            // a wave with more rows left gets a higher priority.
+            if (FS_PRIO == 2) {
+                // static, inverted age rank: the SIMD arbiter favours older waves on ties, so
+                // the younger waves (higher wave index) get the higher priority
+                const uint32_t rank = __builtin_amdgcn_readfirstlane(wave) >> 2;
+                if (rank == 3) __builtin_amdgcn_s_setprio(3);
+                else if (rank == 2) __builtin_amdgcn_s_setprio(2);
+                else if (rank == 1) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            } else if (FS_PRIO) {
+                const int left4 = (4 * (T.Rp - r0)) / max(T.Rp, 1);  // 4 .. 1
+                if (left4 >= 4) __builtin_amdgcn_s_setprio(3);
+                else if (left4 == 3) __builtin_amdgcn_s_setprio(2);
+                else if (left4 == 2) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+        };
+        // general block: per-row fast/slow (scalar), header capture for rows <= Rh (scalar),
+        // clamped refill addresses
+        auto block = [&](int r0, auto refill_tag) {
+            constexpr bool kRefill = decltype(refill_tag)::value;
+            prio(r0);
 #pragma unroll
-                for (int i = 0; i < kPrefetch; ++i) {
-                    const int r = r0 + i;
-                    const int rel = T.rel0 + kRowDwords * r;
-                    const bool fast = (r >= T.RF_lo) && (r <= T.RF_hi);  // wave-uniform (scalar)
-                    if (kHdr) capture_header(lds, gslot, rel, T.lo, pf[i]);
-                    // consume the ring slot, then refill the SAME registers: no copy of an
-                    // in-flight load, so the compiler keeps kPrefetch-1 loads outstanding
-                    process_row(lds, keys, pf[i], rel, fast, M, T.lo, A, cs);
-                    if (kRefill && FS_DIAG != 3) pf[i] = load_chunk(T.gfb, rel + kRowDwords * kPrefetch, T.lo);
-                }
+            for (int i = 0; i < kPrefetch; ++i) {
+                const int r = r0 + i;
+                const int rel = T.rel0 + kRowDwords * r;
+                const bool fast = (r >= T.RF_lo) && (r <= T.RF_hi);  // wave-uniform (scalar)
+                if (r <= T.Rh) capture_header(lds, hb, rel, T.lo, pf[i]);
+                // consume the ring slot, then refill the SAME registers: no copy of an
+                // in-flight load, so the compiler keeps kPrefetch-1 loads outstanding
+                process_row(lds, keys, pf[i], rel, fast, M, T.lo, A, cs);
+                if (kRefill && FS_DIAG != 3) pf[i] = load_chunk(T.gfb, rel + kRowDwords * kPrefetch, T.lo);
+            }
+        };
+        // lean block: every row fast for every lane; the refills of a fast row's successors
+        // lie inside the frame, so they need no clamp: one pointer per block, immediate
+        // row offsets
+        auto lean_block = [&](int r0) {
+            prio(r0);
+            const uint32_t* pb = T.gfb + (T.rel0 + kRowDwords * (r0 + kPrefetch));
+#pragma unroll
+            for (int i = 0; i < kPrefetch; ++i) {
+                process_row(lds, keys, pf[i], 0, true, M, 0, A, cs);
+                if (FS_DIAG != 3) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
+                // keep consume/refill interleaved per row: unfenced, the scheduler sinks all
+                // refills to the block end behind a vmcnt(0), draining the ring every block
+                __builtin_amdgcn_sched_barrier(0);
             }
         };
         using Yes = std::true_type;
         using No = std::false_type;
-        Parsed P = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0};
-        const bool parser = T.fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
         const int Rc = T.Rp - kPrefetch;
         if (T.Rp > 0) {
-            const int ra = min(T.Rsplit, Rc);
-            stream_rows(0, ra, Yes(), Yes());
-            if (T.Rsplit <= Rc && parser) P = parse_frame(lds, gslot, T.sa, T.len, mtu);
-            stream_rows(ra, Rc, No(), Yes());
-            stream_rows(Rc, T.Rp, Yes(), No());
-            if (T.Rsplit > Rc && parser) P = parse_frame(lds, gslot, T.sa, T.len, mtu);
-        } else if (parser) {
-            P = parse_frame(lds, gslot, T.sa, T.len, mtu);  // only sub-4-byte frames: rejected by len
+            // blocks: [head: general] [body: lean] [tail: general] [last: general, no refill],
+            // as three loops in sequence (one code path per loop keeps the ring registers fixed)
+            // (a block is lean only past Rh, so the header rows are always in general blocks)
+            int r0 = 0;
+            for (; r0 < Rc && !(r0 > T.Rh && r0 >= T.RF_lo && r0 + kPrefetch - 1 <= T.RF_hi); r0 += kPrefetch) {
+                block(r0, Yes());
+                if (T.Rh >= r0 && T.Rh < r0 + kPrefetch) parse();
+            }
+            for (; r0 < Rc && r0 + kPrefetch - 1 <= T.RF_hi; r0 += kPrefetch) lean_block(r0);
+            for (; r0 < Rc; r0 += kPrefetch) block(r0, Yes());
+            block(Rc, No());
+            if (T.Rh >= Rc) parse();
+        } else {
+            parse();  // no rows (every frame of the tile under 4 bytes): rejected by length
         }
         FS_STAMP(2);
         // the last ring slot holds the frame's final row: stash it for the padding sum
@@ -628,33 +711,39 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         if (gl == 3u) Y = U;
         Y ^= dpp_quad<kQuadXor1>(Y);
         Y ^= dpp_quad<kQuadXor2>(Y);
-        const uint32_t tpad = (4u - T.te) & 3u;  // zero bytes appended by the dword rounding
-        const uint32_t C = zplain(lds, Y, kLdsZfin + 4096u * tpad);
         // checksum partial sum over the 4 lanes of the group (each < 2^30: no u32 overflow)
         cs += dpp_quad<kQuadXor1>(cs);
         cs += dpp_quad<kQuadXor2>(cs);
-        uint32_t crcv = C;
         const uint64_t csum = cs;
 
         FS_STAMP(3);
-        // ---- the group's lane 0: finish and store.
+        // ---- the group's lane 0: finish and store (its frame's state comes back from LDS).
         if (parser) {
-            if (T.len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
+            uint64_t fS;
+            uint32_t flen;
+            const Parsed P = unpark_parsed(lds, hb, fS, flen);
+            const uint64_t fE = fS + flen, fsdw = fS >> 2;
+            const uint32_t fsa = (uint32_t)(fS & 3u), fte = (uint32_t)(fE & 3u) ? (uint32_t)(fE & 3u) : 4u;
+            const uint32_t fnd = flen >= 4u ? (uint32_t)(((fE + 3u) >> 2) - fsdw) : 0u;
+            const uint32_t fi = tile * kFramesPerTile + grp;
+            uint32_t crcv;
+            if (flen < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
                 uint32_t c = 0xffffffffu;
-                const uint8_t* fbytes = frames + T.E - T.len;
-                for (uint32_t p = 0; p < T.len; ++p)
+                const uint8_t* fbytes = frames + fS;
+                for (uint32_t p = 0; p < flen; ++p)
                     c = lds32(lds, kLdsZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
                 crcv = ~c;
             } else {
-                crcv = ~crcv;
+                const uint32_t tpad = (4u - fte) & 3u;  // zero bytes appended by the dword rounding
+                crcv = ~zplain(lds, Y, kLdsZfin + 4096u * tpad);
             }
             uint32_t verdict = P.verdict, l4 = 0u;
             if (P.compute) {
-                const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + T.sdw * 4u);
-                l4 = finish_l4(lds, stash, fb, T.sa, T.len, T.nd, P, csum, verdict);
+                const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + fsdw * 4u);
+                l4 = finish_l4(lds, stash, fb, fsa, flen, fnd, P, csum, verdict);
             }
-            out[T.fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
-            if (status) status[T.fi] = (uint8_t)verdict;
+            out[fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
+            if (status) status[fi] = (uint8_t)verdict;
         }
         FS_STAMP(4);
         FS_RTSTAMP(6);
@@ -662,8 +751,10 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         if (tile < ntiles) {  // next tile: descriptors, geometry, row prefetch
             tile_descriptors(T, tile, grp, n, offsets, lengths, S);
             tile_geometry(T, S, gl, frames);
+            if (T.Rp > 0) {
 #pragma unroll
-            for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
+                for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
+            }
         }
     }
 }
