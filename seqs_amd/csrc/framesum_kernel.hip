@@ -51,9 +51,6 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_PREFETCH
 #define FS_PREFETCH 6
 #endif
-#ifndef FS_DMA_FIRST
-#define FS_DMA_FIRST 1  // 1: table LDS-DMA before the descriptors (ahead of the first rows)
-#endif
 #ifndef FS_NT
 #define FS_NT 0  // 1: non-temporal row loads
 #endif
@@ -61,7 +58,7 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FS_PRIO 1  // progress-based s_setprio in the row loop (see stream_rows)
 #endif
 #ifndef FS_DIAG
-#define FS_DIAG 0  // diagnostic builds only: 2 = no CRC lookups in the row loop, 3 = no row loads after the prefetch, 4 = no table fill (wrong results)
+#define FS_DIAG 0  // diagnostic builds only: 2 = no CRC lookups in the row loop, 3 = no row loads after the prefetch (wrong results)
 #endif
 
 constexpr int kWave = 64;
@@ -81,7 +78,8 @@ constexpr uint32_t kHdrWaveBytes = kHdrSlotBytes * kFramesPerTile;
 constexpr int kStashBytes = 68;             // the frame's last row (Ethernet padding source); 17-dword stride
 constexpr int kFastRel0 = 2;                // rows whose chunks start at dword >= 2 carry no head/init mask
 
-// LDS map (bytes). [0, 88 KB) is FsTables verbatim (filled by LDS-DMA).
+// LDS map (bytes). [0, 100 KB) is the FsTables LDS image: region A built in place from
+// the Z64 basis, the plain tables copied by LDS-DMA.
 constexpr uint32_t kLdsZ32 = 65536;
 constexpr uint32_t kLdsZ16 = kLdsZ32 + 4096;
 constexpr uint32_t kLdsZfin = kLdsZ16 + 4096;  // Z4, Z3, Z2, Z1 (4 KB each)
@@ -94,9 +92,10 @@ constexpr uint32_t kLdsStash = kLdsHdr + kWavesPerBlock * kHdrWaveBytes;
 constexpr uint32_t kLdsBytes = kLdsStash + kWavesPerBlock * kFramesPerTile * kStashBytes;
 static_assert(kLdsHdr % 16 == 0 && kLdsStash % 16 == 0, "slots must be 16-B aligned");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
-static_assert(sizeof(FsTables) == kLdsTables, "FsTables is the LDS image of the tables");
-constexpr uint32_t kTableChunks = kLdsTables / 1024;  // 1-KB LDS-DMA pieces
-constexpr uint32_t kDmaPerWave = (kTableChunks + kWavesPerBlock - 1) / kWavesPerBlock;
+static_assert(kTablesLdsBytes == kLdsTables, "FsTables is the LDS image of the tables");
+constexpr uint32_t kPlainChunk0 = 65536 / 1024;                     // first 1-KB piece of the plain tables
+constexpr uint32_t kPlainChunks = (kLdsTables - 65536) / 1024;      // 36 pieces
+constexpr uint32_t kDmaPerWave = (kPlainChunks + kWavesPerBlock - 1) / kWavesPerBlock;
 
 #ifdef FS_STAMPS
 // Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
@@ -120,7 +119,6 @@ __device__ unsigned long long g_fs_stamps[8192 * 16];
 #define FS_RTSTAMP(k) do { } while (0)
 #endif
 
-constexpr uint32_t kZ4Off = 128;  // Z4 copies sit in slots 32..63 of each region-A entry row
 
 // DPP quad_perm controls.
 constexpr int kQuadXor1 = 0xB1;  // [1,0,3,2]
@@ -458,8 +456,16 @@ __device__ __forceinline__ void tile_descriptors(Tile& T, uint32_t tile, uint32_
     // then use a longest frame of the tile, see tile_geometry; `frames` itself may lie
     // outside the allocation: the host-staged path passes staging - first offset)
     const uint32_t fl = T.fvalid ? T.fi : n - 1u;
-    S = offsets[fl];
-    T.len = lengths[fl];
+    // Inline asm: hipcc otherwise sinks the loads into their first use (past the region-A
+    // build and the tile branch), serializing two HBM round trips. The values are tied to
+    // an explicit wait (descriptors_ready) before use.
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(S) : "v"(offsets + fl));
+    asm volatile("global_load_dword %0, %1, off" : "=v"(T.len) : "v"(lengths + fl));
+}
+
+// vmcnt(0) tied to the descriptor registers, so no use of them is scheduled above it.
+__device__ __forceinline__ void descriptors_ready(Tile& T, uint64_t& S) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(S), "+v"(T.len));
     if (!T.fvalid) T.len = 0;
 }
 
@@ -521,17 +527,53 @@ __device__ __forceinline__ void tile_geometry(Tile& T, uint64_t S, uint32_t gl, 
     T.RF_hi = group_reduce<false>(fhi);
 }
 
-// The tables' LDS image by LDS-DMA: exactly kDmaPerWave 1-KB pieces per wave (a static
-// count; surplus pieces re-copy the last chunk with identical bytes).
-__device__ __forceinline__ void table_dma(const FsTables* __restrict__ tabs, char* lds, uint32_t wave, uint32_t lane) {
+// Region A in place: thread t builds Z64[b][e] (b = t >> 8, e = t & 255) as the XOR of
+// the basis columns of e's set bits and stores its 8 copies (32 contiguous bytes).
+// The basis row comes in by a scalar load (lgkmcnt), so waiting for it never waits for the
+// descriptors' vector loads issued before it.
+__device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs, char* lds) {
+    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    const uint32_t t = threadIdx.x;
+    const uint32_t b = __builtin_amdgcn_readfirstlane(t >> 8);  // wave-uniform (64 | 256)
+    const uint32_t e = t & 255u;
+    const uint64_t a = reinterpret_cast<uint64_t>(&tabs->z64_basis[b][0]);
+    const uint64_t sa = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    u32x8 basis;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(basis) : "s"(sa));
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t m = 0u - ((e >> j) & 1u);
+        v ^= basis[j] & m;
+    }
+    u32x4* dst = reinterpret_cast<u32x4*>(lds + e * 256u + 32u * b);
+    dst[0] = u32x4{v, v, v, v};
+    dst[1] = u32x4{v, v, v, v};
+}
+
+// The plain tables by LDS-DMA: exactly kDmaPerWave 1-KB pieces per wave (surplus pieces
+// re-copy the last one with identical bytes). Inline asm, invisible to hipcc's vmcnt model
+// (the builtin makes it drain later LDS reads with vmcnt(0)); unknown VMEM ops only make
+// the compiler's own counted waits stricter. Waited for explicitly before the barrier.
+// (m0 is reserved to the compiler: this kernel sets it nowhere else, checked in the asm)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, char* lds, uint32_t wave, uint32_t lane) {
+    typedef __attribute__((address_space(3))) char lds_char;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)lds;
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
-    for (uint32_t k = 0; k < (FS_DIAG == 4 ? 0u : kDmaPerWave); ++k) {
-        const uint32_t c = min(w0 + k * kWavesPerBlock, kTableChunks - 1u);
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
-                                         lds + c * 1024u, 16, 0, 0);
+    for (uint32_t k = 0; k < kDmaPerWave; ++k) {
+        const uint32_t c = kPlainChunk0 + min(w0 + k * kWavesPerBlock, kPlainChunks - 1u);
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                     :
+                     : "v"(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u),
+                       "s"(__builtin_amdgcn_readfirstlane(lds0 + c * 1024u))
+                     : "memory", "m0");
     }
 }
+#pragma clang diagnostic pop
 
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
@@ -570,16 +612,18 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     // the DMA (L2 hits) then overlaps the rows' HBM latency. hipcc does not count LDS-DMA
     // in its vmcnt model: the DMA is issued last and drained with an explicit vmcnt(0),
     // which the first row needs anyway.
+    // Preamble: the first tile's descriptors (the first memory ops, one round trip) while
+    // region A is built in place by VALU; geometry; the plain tables' LDS-DMA (36 KB, L2
+    // hits); the row prefetch; one barrier once this wave's table pieces have landed.
     uint32_t tile = gwave;
     FS_RTSTAMP(5);
     FS_STAMP(0);
     Tile T;
     uint64_t S;
     u32x4 pf[kPrefetch];
-#if FS_DMA_FIRST
-    table_dma(tabs, lds, wave, lane);
-#endif
     tile_descriptors(T, tile, grp, n, offsets, lengths, S);
+    build_region_a(tabs, lds);
+    descriptors_ready(T, S);
 #if defined(FS_STAMPS) && FS_STAMPS == 2
     __builtin_amdgcn_s_waitcnt(0x0f70);  // fine-stamp build only: time the descriptor round trip
     FS_STAMP(8);
@@ -588,24 +632,20 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     if (__builtin_amdgcn_readfirstlane(tile) < ntiles) {
         tile_geometry(T, S, gl, frames);
         rows0 = T.Rp > 0;
-        if (rows0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
+    }
+    plain_dma(tabs, lds, wave, lane);
+    if (rows0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-            for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
-        }
+        for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
     }
     FS_STAMP(9);
-#if !FS_DMA_FIRST
-    table_dma(tabs, lds, wave, lane);
-#endif
-#if FS_DMA_FIRST
-    // the table pieces are older than the rows
-    if (rows0) __builtin_amdgcn_s_waitcnt(0x0f70 | kPrefetch);
-    else __builtin_amdgcn_s_waitcnt(0x0f70);
-#else
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): table pieces and the first rows
-#endif
+    // the table pieces are older than the rows: vmcnt(kPrefetch) (vmcnt(0) without rows);
+    // lgkmcnt(0): this wave's region-A stores
+    // s_waitcnt field layout (gfx9): vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4], lgkmcnt[11:8]
+    if (rows0) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
+    else __builtin_amdgcn_s_waitcnt(0x0070);
     FS_STAMP(10);
-    __builtin_amdgcn_s_barrier();  // LDS tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     FS_STAMP(1);
 
     while (tile < ntiles) {
@@ -705,7 +745,7 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
 
         // ---- combine the 16 streams of each frame: C = Z_(4-t)( xor_l Z_16(3-l)( U_l ) ),
         //      U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3   (3 dependent LDS round trips).
-        const uint32_t U = zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zrep(lds, A[2], keys, kZ4Off) ^ A[3];
+        const uint32_t U = zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3];
         const uint32_t ybase = (gl == 0u) ? kLdsZ48 : (gl == 1u) ? kLdsZ32 : kLdsZ16;
         uint32_t Y = zplain(lds, U, ybase);
         if (gl == 3u) Y = U;
@@ -750,6 +790,7 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         tile += nwaves;
         if (tile < ntiles) {  // next tile: descriptors, geometry, row prefetch
             tile_descriptors(T, tile, grp, n, offsets, lengths, S);
+            descriptors_ready(T, S);
             tile_geometry(T, S, gl, frames);
             if (T.Rp > 0) {
 #pragma unroll

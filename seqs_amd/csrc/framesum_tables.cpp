@@ -38,15 +38,21 @@ void build_tables(FsTables* t) {
     std::memset(t, 0, sizeof(*t));
     uint32_t t1[256];
     byte_table(t1);
-    static uint32_t zrow[4][256], z4[4][256];
+    static uint32_t zrow[4][256];
     op_table(t1, 64, zrow);
-    op_table(t1, 4, z4);
     for (uint32_t e = 0; e < 256; ++e)
         for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t c = 0; c < 8; ++c) {
-                t->region_a[e][8 * b + c] = zrow[b][e];
-                t->region_a[e][32 + 8 * b + c] = z4[b][e];
-            }
+            for (uint32_t c = 0; c < 8; ++c) t->region_a[e][8 * b + c] = zrow[b][e];
+    for (uint32_t b = 0; b < 4; ++b)
+        for (uint32_t j = 0; j < 8; ++j) t->z64_basis[b][j] = zrow[b][1u << j];
+    // region A entries are the XOR of the basis columns of their set bits (GF(2) linearity)
+    for (uint32_t b = 0; b < 4; ++b)
+        for (uint32_t e = 0; e < 256; ++e) {
+            uint32_t v = 0;
+            for (uint32_t j = 0; j < 8; ++j)
+                if ((e >> j) & 1u) v ^= t->z64_basis[b][j];
+            if (v != zrow[b][e]) throw std::logic_error("Z_64 basis mismatch");
+        }
     op_table(t1, 32, t->z32);
     op_table(t1, 16, t->z16);
     for (int k = 0; k < 4; ++k) op_table(t1, 4 - k, t->zfin[k]);

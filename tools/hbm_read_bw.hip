@@ -110,6 +110,10 @@ int main(int argc, char** argv) {
     }
     const uint32_t fl = 1500, nf = (uint32_t)(nbytes / fl);
 #define FR(PF, G, NT, GRID, NAME) timeit([&](int i) { hipLaunchKernelGGL((k_frames<PF, G, NT>), dim3(GRID), dim3(1024), 0, 0, bufs[i % NB], nf, fl, out); }, NAME)
+    FR(6, 1, false, cus, "frames G=1  PF=6");
+    FR(8, 1, false, cus, "frames G=1  PF=8");
+    FR(12, 1, false, cus, "frames G=1  PF=12");
+    FR(6, 2, false, cus, "frames G=2  PF=6");
     FR(6, 4, false, cus, "frames G=4  PF=6");
     FR(6, 4, true, cus, "frames G=4  PF=6 nt");
     FR(4, 16, false, cus, "frames G=16 PF=4");
