@@ -8,33 +8,38 @@
 //
 // Work decomposition:
 //   * a wave owns a TILE of 16 frames; each frame gets a 4-lane GROUP.
-//   * a frame is cut into 64-byte ROWS anchored at its (dword-rounded) END, so
-//     the head row is the partial one; lane l of the group loads dwords
-//     [4l, 4l+4) of every row with one global_load_dwordx4 (16 B/lane), kPrefetch
-//     rows ahead. The row loop depends only on the frame descriptor (offset,
-//     length); the frame's first 128 bytes are fetched into LDS by LDS-DMA next to
-//     the first rows, and the header parse runs after the first block of rows,
-//     hidden behind the rows in flight.
+//   * a frame is cut into 64-byte ROWS anchored at its (dword-rounded) END, so the
+//     head row is the partial one; lane l of the group loads dwords [4l, 4l+4) of
+//     every row with one global_load_dwordx4 (16 B/lane), kPrefetch rows ahead.
+//   * LEAN rows: every row except the first H of a tile (H = 1 or 2 for a batch of
+//     equal lengths) is consumed with no per-row mask at all. The head rows (bytes
+//     before the frame, the CRC init on frame dwords 0/1) take the masked path. The
+//     up to 3 bytes past the frame end that the dword rounding reads are not masked
+//     in the loop: their CRC contribution is XOR-ed out of the combine and their sum
+//     subtracted at the finish (both linear).
 //   * CRC: each lane keeps 4 independent dword STREAMS; a stream's successive
 //     dwords are 64 B apart, so its Horner step is  A <- Z64(A) ^ w  with Z64 a
 //     fixed GF(2) linear map evaluated by 4 byte-table lookups in LDS. After the
 //     last row the 16 streams of a frame are combined in 3 dependent lookups
 //     (U = Z12(A0)^Z8(A1)^Z4(A2)^A3 per lane, Z_(16(3-l)) per lane l + DPP
 //     quad xor, then a final Z_(4-t) that also removes the t <= 3 zero bytes
-//     the dword rounding appended). Leading zero rows do not change a zero-init CRC; the CRC init
-//     is applied by XOR-ing the frame's first 4 bytes with 0xFF.
+//     the dword rounding appended). Leading zero rows do not change a zero-init CRC; the
+//     CRC init is applied by XOR-ing the frame's first 4 bytes with 0xFF.
 //   * one's-complement sum: the same registers feed v_sad_u16 (acc += lo16 + hi16,
 //     one op per dword; congruent mod 65535 to the byte-swapped big-endian word
-//     sum) over every frame byte; the group's lane 0 subtracts, in the same
-//     domain, the Ethernet + IP header bytes, the excluded words and the Ethernet
-//     padding and adds the pseudo-header, then folds with a
-//     positive offset so RecvEth's Sum16 result (incl. the 0x0000 / 0xFFFF edge)
-//     is reproduced bit for bit.
-//   * LDS tables: the hot Z64 (and Z4) tables are stored as 8 copies per table
-//     in a [entry][table*8+copy] layout, 256 B per entry. Lane L = c + 8h of a
-//     32-lane bank group reads table (k+h)&3 in its k-th lookup, so the 32
-//     lanes hit 32 distinct banks: conflict-free ds_read_b32 for any data.
-//     One v_perm_b32 forms the LDS address (entry byte | per-lane slot byte).
+//     sum) over every frame byte; the header parse computes, in the same domain,
+//     the sums of the Ethernet + IP header bytes, of the excluded words and of the
+//     Ethernet padding (vectorised over the group's 4 lanes) and the pseudo-header,
+//     and the finish folds with a positive offset so RecvEth's Sum16 result (incl.
+//     the 0x0000 / 0xFFFF edge) is reproduced bit for bit.
+//   * the frame's first 32 dwords reach a per-group LDS header slot by dword LDS-DMA
+//     issued with the tile's first rows (no per-row header capture); the parse runs
+//     after the first block of rows, behind the ring's loads.
+//   * LDS tables: the hot Z64 table is stored as 8 copies per byte table in an
+//     [entry][table*8+copy] layout, 256 B per entry. Lane L = c + 8h of a 32-lane
+//     bank group reads table (k+h)&3 in its k-th lookup, so the 32 lanes hit 32
+//     distinct banks: conflict-free ds_read_b32 for any data. One v_perm_b32 forms
+//     the LDS address (entry byte | per-lane slot byte).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -51,14 +56,8 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_PREFETCH
 #define FS_PREFETCH 6
 #endif
-#ifndef FS_NT
-#define FS_NT 0  // 1: non-temporal row loads
-#endif
 #ifndef FS_PRIO
-#define FS_PRIO 1  // progress-based s_setprio in the row loop (see stream_rows)
-#endif
-#ifndef FS_DIAG
-#define FS_DIAG 0  // diagnostic builds only: 2 = no CRC lookups in the row loop, 3 = no row loads after the prefetch (wrong results)
+#define FS_PRIO 1  // progress-based s_setprio per block of rows
 #endif
 
 constexpr int kWave = 64;
@@ -67,16 +66,14 @@ constexpr int kThreads = kWave * kWavesPerBlock;
 constexpr int kFramesPerTile = 16;
 constexpr int kRowDwords = 16;
 constexpr int kPrefetch = FS_PREFETCH;
-// Header slots: the row loop writes every loaded 16-B chunk that holds frame dwords [0, 28)
-// into the group's slot, at the dwords it was loaded from (a clamped head chunk lands at the
-// frame start; its bytes before the frame go to the slot's 16-B guard). Slots are 36 dwords
-// apart, so the 8 parser lanes of a 32-lane bank group read distinct banks.
-constexpr int kHdrDwords = 28;
-constexpr uint32_t kHdrSlotBytes = 144;
-static_assert(kHdrSlotBytes >= 16 + 4 * (kHdrDwords + 3) + 4, "slot holds the guard + the last chunk");
-constexpr uint32_t kHdrWaveBytes = kHdrSlotBytes * kFramesPerTile;
-constexpr int kStashBytes = 68;             // the frame's last row (Ethernet padding source); 17-dword stride
-constexpr int kFastRel0 = 2;                // rows whose chunks start at dword >= 2 carry no head/init mask
+
+// Header slots: frame dwords [0, 32) of each group's frame, written by 8 dword LDS-DMA
+// instructions per wave in the layout [x >> 2][group][x & 3] (256 B per instruction),
+// so the DMA destination is lane-linear and both the parser lanes (one per group, same x)
+// and the group-vectorised sums (lane gl reads x = 4i + gl) read conflict-free.
+constexpr int kHdrDwords = 32;
+constexpr int kHdrDmas = kHdrDwords / 4;
+constexpr uint32_t kHdrWaveBytes = 4u * kHdrDwords * kFramesPerTile;  // 2 KB
 
 // LDS map (bytes). [0, 100 KB) is the FsTables LDS image: region A built in place from
 // the Z64 basis, the plain tables copied by LDS-DMA.
@@ -88,9 +85,7 @@ constexpr uint32_t kLdsZ12 = kLdsZ48 + 4096;
 constexpr uint32_t kLdsZ8 = kLdsZ12 + 4096;
 constexpr uint32_t kLdsTables = kLdsZ8 + 4096;
 constexpr uint32_t kLdsHdr = kLdsTables;
-constexpr uint32_t kLdsStash = kLdsHdr + kWavesPerBlock * kHdrWaveBytes;
-constexpr uint32_t kLdsBytes = kLdsStash + kWavesPerBlock * kFramesPerTile * kStashBytes;
-static_assert(kLdsHdr % 16 == 0 && kLdsStash % 16 == 0, "slots must be 16-B aligned");
+constexpr uint32_t kLdsBytes = kLdsHdr + kWavesPerBlock * kHdrWaveBytes;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kTablesLdsBytes == kLdsTables, "FsTables is the LDS image of the tables");
 constexpr uint32_t kPlainChunk0 = 65536 / 1024;                     // first 1-KB piece of the plain tables
@@ -119,7 +114,6 @@ __device__ unsigned long long g_fs_stamps[8192 * 16];
 #define FS_RTSTAMP(k) do { } while (0)
 #endif
 
-
 // DPP quad_perm controls.
 constexpr int kQuadXor1 = 0xB1;  // [1,0,3,2]
 constexpr int kQuadXor2 = 0x4E;  // [2,3,0,1]
@@ -145,16 +139,16 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
-// Z(a) ^ w with Z from replicated region A (off = 0: Z64, off = 128: Z4). Conflict-free.
-__device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const LaneKeys& k, uint32_t off, uint32_t w = 0u) {
-    uint32_t t0 = lds32(lds, off + __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
-    uint32_t t1 = lds32(lds, off + __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
-    uint32_t t2 = lds32(lds, off + __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
-    uint32_t t3 = lds32(lds, off + __builtin_amdgcn_perm(a, k.cvec, k.sel[3]));
+// Z64(a) ^ w from replicated region A. Conflict-free.
+__device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const LaneKeys& k, uint32_t w) {
+    uint32_t t0 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
+    uint32_t t1 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
+    uint32_t t2 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
+    uint32_t t3 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[3]));
     return xor3(xor3(t0, t1, t2), t3, w);
 }
 
-// Z operator from a plain [4][256] table (region B; a few uses per frame).
+// Z operator from a plain [4][256] table (a few uses per frame).
 __device__ __forceinline__ uint32_t zplain(const char* lds, uint32_t a, uint32_t base) {
     return lds32(lds, base + ((a & 0xffu) << 2)) ^ lds32(lds, base + 1024 + (((a >> 8) & 0xffu) << 2)) ^
            lds32(lds, base + 2048 + (((a >> 16) & 0xffu) << 2)) ^ lds32(lds, base + 3072 + ((a >> 24) << 2));
@@ -167,137 +161,127 @@ __device__ __forceinline__ uint32_t dpp_quad(uint32_t v) {
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); }
 
-// 16 bytes of row data for one lane: dwords [rel, rel+4) relative to the frame's
-// first dword. Issued unconditionally (no divergent branch around the load, so
-// the prefetch ring keeps kPrefetch-1 loads in flight); rows that start before
-// the frame are clamped to `lo` (the frame's first chunk, never below the buffer
-// start) and realigned / masked by the slow path. Rows never run past the frame's last dword (see the segments).
-__device__ __forceinline__ u32x4 load_chunk(const uint32_t* fb, int rel, int lo) {
-    const u32x4_a4* p = reinterpret_cast<const u32x4_a4*>(fb + max(rel, lo));
-    if (FS_NT) return __builtin_nontemporal_load(p);  // streamed once: no reuse in L2
-    return *p;
-}
-
 // One's-complement accumulation: v_sad_u16(x, 0, acc) = acc + x[15:0] + x[31:16] in ONE op.
 // x[15:0] + x[31:16] is congruent to the dword's native little-endian value mod 65535 and
-// is 0 iff the dword is 0, which is all Sum16's fold needs. A lane adds at
-// most 4096 dwords of a 64-KiB frame (< 2^30), so the 32-bit accumulator cannot wrap.
+// is 0 iff the dword is 0, which is all Sum16's fold needs. It is linear
+// over disjoint byte masks (no carry crosses a byte). A lane adds at most 2^15 dwords of a
+// frame under 512 KiB, each < 2^17, so the 32-bit accumulator cannot wrap there.
 __device__ __forceinline__ uint32_t sad16(uint32_t x, uint32_t acc) { return __builtin_amdgcn_sad_u16(x, 0u, acc); }
 
-// Per-frame row parameters, held by every lane of the frame's group.
-struct RowMasks {
-    int nd;              // frame dwords (incl. the partial last one); 0 = nothing to stream
-    uint32_t head_mask;  // bytes of dword 0 inside the frame; also the CRC init's part in dword 0
-    uint32_t init1;      // the CRC init's part in dword 1
-    uint32_t tail_mask;  // bytes of dword nd-1 inside the frame
-};
-
-__device__ __forceinline__ void process_row(char* lds, const LaneKeys& keys, u32x4 v, int rel, bool fast,
-                                            const RowMasks& m, int lo, uint32_t (&A)[4], uint32_t& cs) {
-    if (FS_DIAG == 2) {
-        A[0] ^= v.x; A[1] ^= v.y; A[2] ^= v.z; A[3] ^= v.w;
-        cs = sad16(v.x, cs); cs = sad16(v.y, cs); cs = sad16(v.z, cs); cs = sad16(v.w, cs);
-        return;
-    }
-    if (fast) {
-        A[0] = zrep(lds, A[0], keys, 0, v.x);
-        A[1] = zrep(lds, A[1], keys, 0, v.y);
-        A[2] = zrep(lds, A[2], keys, 0, v.z);
-        A[3] = zrep(lds, A[3], keys, 0, v.w);
-        cs = sad16(v.x, cs);
-        cs = sad16(v.y, cs);
-        cs = sad16(v.z, cs);
-        cs = sad16(v.w, cs);
-    } else {
-        const int sh = max(rel, lo) - rel;  // >0 only for a clamped row that starts before the frame
-        if (sh > 0 && sh < 4) {
-            const u32x4 u = v;
-            v.w = (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
-            v.z = (sh == 1) ? u.y : (sh == 2) ? u.x : 0u;
-            v.y = (sh == 1) ? u.x : 0u;
-            v.x = 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int rj = rel + j;
-            uint32_t d = (rj >= 0) ? v[j] : 0u;
-            uint32_t x = 0u;
-            if (rj == 0) { d &= m.head_mask; x = m.head_mask; }
-            if (rj == 1) x = m.init1;
-            if (rj == m.nd - 1) d &= m.tail_mask;
-            A[j] = zrep(lds, A[j], keys, 0, d ^ x);
-            cs = sad16(d, cs);
-        }
-    }
-}
-
-// ---- parser-lane helpers over the LDS header slot (absolute-dword aligned: slot
-// dword k = the frame's dword k counted from its first dword, frame byte p at slot byte
-// 16 + sa + p). `hb` = the group's slot.
-__device__ __forceinline__ uint32_t hdr_dw(const char* lds, uint32_t hb, uint32_t k) {
-    return lds32(lds, hb + 16u + 4u * k);
-}
-
-// Row data -> header slot: the chunk's 16 bytes are frame dwords [p, p+4), p = max(rel, lo).
-__device__ __forceinline__ void capture_header(char* lds, uint32_t hb, int rel, int lo, u32x4 v) {
-    const int p = max(rel, lo);
-    if (p < kHdrDwords) *reinterpret_cast<u32x4*>(lds + hb + 16u + 4u * (uint32_t)p) = v;
-}
-// frame bytes [4j, 4j+4) as a little-endian dword
-__device__ __forceinline__ uint32_t frame_dw(const char* lds, uint32_t hb, uint32_t sa, uint32_t j) {
-    return __builtin_amdgcn_alignbyte(hdr_dw(lds, hb, j + 1), hdr_dw(lds, hb, j), sa);
-}
 // bytes of absolute dword k that lie in the absolute byte range [a0, a1)
 __device__ __forceinline__ uint32_t range_mask(int k, int a0, int a1) {
     const int lo = min(max(a0 - 4 * k, 0), 4), hi = min(max(a1 - 4 * k, 0), 4);
-    const uint32_t mhi = (hi >= 4) ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
-    const uint32_t mlo = (lo >= 4) ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
-    return mhi & ~mlo;
+    const uint32_t m = (0xffffffffu >> (32 - 8 * (hi - lo))) << (8 * lo);
+    return hi > lo ? m : 0u;
 }
-// sum, in the accumulator's 16-bit-half domain, of frame bytes [p0, p1) taken from the
-// contiguous stash image whose dword 0 is the frame's dword `d0` (= nd - 16). Bytes outside
-// the image count 0.
-__device__ uint32_t nsum_lds(const char* lds, uint32_t base, int d0, int ndw, uint32_t sa, int p0, int p1) {
-    uint32_t s = 0;
-    if (p1 <= p0) return s;
-    const int a0 = (int)sa + p0, a1 = (int)sa + p1;
-    for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) {
-        const int i = k - d0;
-        if (i >= 0 && i < ndw) s = sad16(lds32(lds, base + 4u * (uint32_t)i) & range_mask(k, a0, a1), s);
+
+// ---------------------------------------------------------------------------------------
+// Rows.
+
+// A lean row: four Z64 steps and four v_sad_u16, no masks.
+__device__ __forceinline__ void lean_row(const char* lds, const LaneKeys& k, u32x4 v, uint32_t (&A)[4], uint32_t& cs) {
+    A[0] = zrep(lds, A[0], k, v.x);
+    A[1] = zrep(lds, A[1], k, v.y);
+    A[2] = zrep(lds, A[2], k, v.z);
+    A[3] = zrep(lds, A[3], k, v.w);
+    cs = sad16(v.x, cs);
+    cs = sad16(v.y, cs);
+    cs = sad16(v.z, cs);
+    cs = sad16(v.w, cs);
+}
+
+// A masked row: the chunk was loaded from frame dword p (= rel unless clamped up, see
+// load_pos); realign it to [rel, rel+4), zero the dwords before the frame, mask the head and
+// tail bytes and apply the CRC init.
+// nd: frame dwords (0 = nothing to stream); sa: S & 3; tail_mask: bytes of dword nd-1 inside
+// the frame. The head mask (bytes of dword 0 inside the frame) is also the CRC init's part in
+// dword 0; its complement is the init's part in dword 1.
+__device__ __forceinline__ void masked_row(const char* lds, const LaneKeys& k, u32x4 u, int rel, int p, int nd,
+                                           uint32_t sa, uint32_t tail_mask, uint32_t (&A)[4], uint32_t& cs) {
+    const uint32_t head_mask = 0xffffffffu << (8u * sa);
+    const int sh = p - rel;  // > 0 only for a clamped chunk; then every dword below p lies before the frame
+    uint32_t v[4];
+    v[0] = u.x;
+    v[1] = (sh == 0) ? u.y : u.x;
+    v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
+    v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int x = rel + j;
+        uint32_t d = (x >= 0) ? v[j] : 0u;
+        uint32_t c = 0u;
+        if (x == 0) { d &= head_mask; c = head_mask; }
+        if (x == 1) c = ~head_mask;
+        if (x == nd - 1) d &= tail_mask;
+        A[j] = zrep(lds, A[j], k, d ^ c);
+        cs = sad16(d, cs);
     }
-    return s;
 }
-// the same over the header image (frame bytes [p0, p1) with p1 <= 4 * kHdrDwords - sa)
-__device__ uint32_t nsum_hdr(const char* lds, uint32_t hb, uint32_t sa, int p0, int p1) {
-    uint32_t s = 0;
-    if (p1 <= p0) return s;
+
+// ---------------------------------------------------------------------------------------
+// Header slot (frame dwords [0, 32) of the group's frame, layout [x>>2][group][x&3]).
+
+__device__ __forceinline__ uint32_t hdr_at(uint32_t hw, uint32_t g, uint32_t x) {
+    return hw + ((x >> 2) << 8) + (g << 4) + ((x & 3u) << 2);
+}
+__device__ __forceinline__ uint32_t hdr_dw(const char* lds, uint32_t hw, uint32_t g, uint32_t x) {
+    return lds32(lds, hdr_at(hw, g, x));
+}
+// frame bytes [4j, 4j+4) as a little-endian dword (slot dwords are absolute, sa = S & 3)
+__device__ __forceinline__ uint32_t frame_dw(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t j) {
+    return __builtin_amdgcn_alignbyte(hdr_dw(lds, hw, g, j + 1), hdr_dw(lds, hw, g, j), sa);
+}
+
+// Sum, in the accumulator's 16-bit-half domain, of frame bytes [p0, p1) held in the slot's
+// first 4*nx dwords, split over the group's 4 lanes (lane gl takes dwords 4i + gl) and
+// totalled over the group by DPP. Every lane of the group calls it with the same arguments.
+__device__ __forceinline__ uint32_t slot_sum(const char* lds, uint32_t hw, uint32_t g, uint32_t gl, uint32_t sa,
+                                             int p0, int p1, int nx) {
     const int a0 = (int)sa + p0, a1 = (int)sa + p1;
-    for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s = sad16(hdr_dw(lds, hb, (uint32_t)k) & range_mask(k, a0, a1), s);
+    uint32_t s = 0;
+    for (int i = 0; i < nx; ++i) {
+        const int x = 4 * i + (int)gl;
+        s = sad16(lds32(lds, hw + ((uint32_t)i << 8) + (g << 4) + (gl << 2)) & range_mask(x, a0, a1), s);
+    }
+    s += dpp_quad<kQuadXor1>(s);
+    s += dpp_quad<kQuadXor2>(s);
     return s;
 }
 
-// Header parse result of one frame (frame lane), computed while its rows stream.
+// exact sum of frame bytes [p0, p1) straight from global memory (rare paths)
+__device__ uint32_t global_sum(const uint32_t* fb, uint32_t sa, int p0, int p1) {
+    uint32_t s = 0;
+    if (p1 <= p0) return s;
+    const int a0 = (int)sa + p0, a1 = (int)sa + p1;
+    for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s = sad16(fb[k] & range_mask(k, a0, a1), s);
+    return s;
+}
+
+// Header parse result of one frame (parser lane), computed while its rows stream.
 struct Parsed {
     uint32_t verdict;   // final unless `compute`
     uint32_t ip_csum;
     uint32_t stored;    // stored L4 checksum (BE)
     int compute;        // the L4 checksum is computed
     int parity;         // absolute parity of the L4 start (1 = odd)
-    uint32_t off, end;  // L4 segment [off, end) (frame-relative); Ethernet padding is [end, len)
-    int64_t corr;       // checksum corrections except the padding (16-bit-half domain)
+    uint32_t off, end;  // L4 segment [off, end) (frame-relative)
+    int64_t corr;       // every checksum correction (16-bit-half domain)
     int64_t corr_fixed; // the pseudo-header and excluded-word part of corr
 };
 
-// Header parse for one frame (frame lane). Gates follow stacks/portstack.go:163-308
+// Header parse for one frame (parser lane). Gates follow stacks/portstack.go:163-308
 // exactly (oracle/framesum_oracle.c restates them line by line; the parity tests
-// compare the two). Reads only the LDS header image.
-__device__ Parsed parse_frame(const char* lds, uint32_t hb, uint32_t sa, uint32_t len, uint32_t mtu) {
+// compare the two). Reads only the LDS header slot; `hsum` = sum of frame bytes [0, off)
+// and `pad` = sum of the Ethernet padding [end, len), both from the group-vectorised sums
+// (pad < 0: the padding lies past the slot, summed here from global memory).
+__device__ __attribute__((noinline)) Parsed parse_frame(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t len, uint32_t mtu,
+                              uint32_t hsum, int64_t pad, const uint32_t* fb) {
     Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0};
     if (len < 34u) { r.verdict = V_SMOL; return r; }                          // portstack.go:167-168
     if (mtu != 0 && len > mtu) { r.verdict = V_MTU; return r; }              // :169-172
     uint32_t bs[9];                                                           // bswap32(frame dword j), j = 3..8
 #pragma unroll
-    for (uint32_t j = 3; j < 9; ++j) bs[j] = __builtin_bswap32(frame_dw(lds, hb, sa, j));
+    for (uint32_t j = 3; j < 9; ++j) bs[j] = __builtin_bswap32(frame_dw(lds, hw, g, sa, j));
     const uint32_t etype = bs[3] >> 16;                                       // headers.go:209-215
     const uint32_t vihl = (bs[3] >> 8) & 0xffu;
     {   // eth/headers.go:333-340 via Put (:289-301): version forced to 4, checksum zeroed, 20 bytes.
@@ -324,9 +308,9 @@ __device__ Parsed parse_frame(const char* lds, uint32_t hb, uint32_t sa, uint32_
     const uint32_t q = (off - 2u) >> 2;
     uint32_t lb[6];
 #pragma unroll
-    for (uint32_t i = 0; i < 6; ++i) lb[i] = __builtin_bswap32(frame_dw(lds, hb, sa, q + i));
+    for (uint32_t i = 0; i < 6; ++i) lb[i] = __builtin_bswap32(frame_dw(lds, hw, g, sa, q + i));
     const uint32_t sport = lb[0] & 0xffffu, dport = lb[1] >> 16;
-    uint32_t lenword, excl;
+    uint32_t lenword;
     if (proto == 17u) {                                                       // :222-244
         if (l4len < 8u) { r.verdict = V_SHORT; return r; }
         const uint32_t ulen = lb[1] & 0xffffu;
@@ -334,7 +318,6 @@ __device__ Parsed parse_frame(const char* lds, uint32_t hb, uint32_t sa, uint32_
         if (ulen < 8u) { r.verdict = V_UDPLEN; return r; }
         lenword = ulen;                                                       // headers.go:386-390
         r.stored = lb[2] >> 16;
-        excl = 6;                                                             // Checksum (2 bytes)
     } else if (proto == 6u) {                                                 // :283-308
         if (l4len < 20u) { r.verdict = V_SHORT; return r; }
         const uint32_t toff = ((lb[3] >> 12) & 0xfu) * 4u;                    // headers.go:477-485
@@ -342,7 +325,6 @@ __device__ Parsed parse_frame(const char* lds, uint32_t hb, uint32_t sa, uint32_
         if (toff < 20u || toff > l4len) { r.verdict = V_TCPOFF; return r; }
         lenword = (tl - ipoff) & 0xffffu;                                     // headers.go:516
         r.stored = lb[4] & 0xffffu;
-        excl = 16;                                                            // Checksum + UrgentPtr (:518-526)
     } else {
         r.verdict = V_PROTO;                                                  // :220-221
         return r;
@@ -350,38 +332,42 @@ __device__ Parsed parse_frame(const char* lds, uint32_t hb, uint32_t sa, uint32_
     r.compute = 1;
     r.off = off;
     r.end = end;
-    // Total over [off, end) = all streamed frame bytes [0, len) + these corrections (+ the
-    // padding correction applied at the end, from the stash), all in the 16-bit-half domain.
-    int64_t t = 0;
-    t -= (int64_t)nsum_hdr(lds, hb, sa, (int)(off + excl), (int)(off + excl + (proto == 6u ? 4u : 2u)));
+    // Total over [off, end) = all streamed frame bytes [0, len) + these corrections, in the
+    // 16-bit-half domain: a big-endian word at frame offset p (even) weighs 256^((sa + p) & 1),
+    // i.e. it enters as itself when the L4 start is odd, byte-swapped when even.
     r.parity = (int)((sa + off) & 1u);
+    const bool odd = r.parity != 0;
+    // excluded words: the stored checksum (UDP headers.go:386-390; TCP :518-526) and, for
+    // TCP, the urgent pointer (:518-526 never adds it)
+    int64_t t = -(int64_t)(odd ? r.stored : bswap16(r.stored));
+    if (proto == 6u) {
+        const uint32_t urg = lb[5] >> 16;
+        t -= (int64_t)(odd ? urg : bswap16(urg));
+    }
     const uint32_t w[6] = {bs[6] & 0xffffu, bs[7] >> 16, bs[7] & 0xffffu, bs[8] >> 16, proto, lenword};
 #pragma unroll
-    for (int i = 0; i < 6; ++i) t += (int64_t)(r.parity ? w[i] : bswap16(w[i]));
+    for (int i = 0; i < 6; ++i) t += (int64_t)(odd ? w[i] : bswap16(w[i]));
     r.corr_fixed = t;
-    t -= (int64_t)nsum_hdr(lds, hb, sa, 0, (int)off);  // the Ethernet + IP header bytes
+    t -= (int64_t)hsum;  // the Ethernet + IP header bytes [0, off)
+    if (end < len) t -= (pad >= 0) ? pad : (int64_t)global_sum(fb, sa, (int)end, (int)len);
     r.corr = t;
     return r;
 }
 
 // The parse result lives in LDS while the rows stream (it would otherwise hold 11 VGPRs
-// across the row loops): dwords 0..13 of the group's header slot, dead after the parse and
-// rewritten only by the next tile's rows, after this tile's finish.
-// The frame's descriptor (offset, length) is parked next to it (dwords 11..13).
-__device__ __forceinline__ void park_parsed(char* lds, uint32_t hb, const Parsed& P, uint64_t S, uint32_t len) {
-    const uint32_t v[14] = {P.verdict, P.ip_csum, P.stored, (uint32_t)P.compute, (uint32_t)P.parity, P.off, P.end,
+// across the row loops): dwords 0..10 of the group's header slot, dead after the parse and
+// rewritten only by the next tile's header DMA, after this tile's finish.
+__device__ __forceinline__ void park_parsed(char* lds, uint32_t hw, uint32_t g, const Parsed& P) {
+    const uint32_t v[11] = {P.verdict, P.ip_csum, P.stored, (uint32_t)P.compute, (uint32_t)P.parity, P.off, P.end,
                             (uint32_t)P.corr, (uint32_t)((uint64_t)P.corr >> 32), (uint32_t)P.corr_fixed,
-                            (uint32_t)((uint64_t)P.corr_fixed >> 32), (uint32_t)S, (uint32_t)(S >> 32), len};
+                            (uint32_t)((uint64_t)P.corr_fixed >> 32)};
 #pragma unroll
-    for (uint32_t k = 0; k < 14; ++k)
-        *reinterpret_cast<uint32_t*>(lds + hb + 16u + 4u * k) = v[k];
+    for (uint32_t k = 0; k < 11; ++k) *reinterpret_cast<uint32_t*>(lds + hdr_at(hw, g, k)) = v[k];
 }
-__device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hb, uint64_t& S, uint32_t& len) {
-    uint32_t v[14];
+__device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, uint32_t g) {
+    uint32_t v[11];
 #pragma unroll
-    for (uint32_t k = 0; k < 14; ++k) v[k] = hdr_dw(lds, hb, k);
-    S = ((uint64_t)v[12] << 32) | v[11];
-    len = v[13];
+    for (uint32_t k = 0; k < 11; ++k) v[k] = hdr_dw(lds, hw, g, k);
     Parsed P;
     P.verdict = v[0];
     P.ip_csum = v[1];
@@ -395,9 +381,9 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hb, ui
     return P;
 }
 
-// Final L4 checksum + verdict (frame lane) once the streamed sum is known.
-__device__ uint32_t finish_l4(const char* lds, uint32_t stash, const uint32_t* fb, uint32_t sa, uint32_t len,
-                              uint32_t nd, const Parsed& P, uint64_t main_sum, uint32_t& verdict) {
+// Final L4 checksum + verdict (parser lane) once the streamed sum is known.
+__device__ uint32_t finish_l4(const uint32_t* fb, uint32_t sa, uint32_t len, const Parsed& P, uint64_t main_sum,
+                              uint32_t& verdict) {
     // Every term is congruent (mod 65535) to its exact native contribution, and the true
     // total is > 0 (the pseudo-header protocol word is 6 or 17), so adding 65535 * 2^20
     // keeps t positive and the fold below lands on the same one's-complement value.
@@ -405,20 +391,7 @@ __device__ uint32_t finish_l4(const char* lds, uint32_t stash, const uint32_t* f
     if (len >= (1u << 19)) {
         // >= 512 KiB frame (only reachable with a huge Ethernet padding): a lane's streamed
         // 32-bit sum may have wrapped, so sum the L4 segment [off, end) exactly from memory.
-        const int a0 = (int)(sa + P.off), a1 = (int)(sa + P.end);
-        uint32_t s = 0;
-        for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s = sad16(fb[k] & range_mask(k, a0, a1), s);
-        t = (int64_t)s + P.corr_fixed + 65535LL * (1LL << 20);
-    } else if (P.end < len) {  // Ethernet padding after the IP datagram
-        const int sd0 = (int)nd - 16;
-        if ((int)(sa + P.end) >= 4 * sd0) {
-            t -= (int64_t)nsum_lds(lds, stash, sd0, 16, sa, (int)P.end, (int)len);
-        } else {  // long padding (malformed frame): exact sum straight from global memory
-            const int a0 = (int)(sa + P.end), a1 = (int)(sa + len);
-            uint32_t s = 0;
-            for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s = sad16(fb[k] & range_mask(k, a0, a1), s);
-            t -= (int64_t)s;
-        }
+        t = (int64_t)global_sum(fb, sa, (int)P.off, (int)P.end) + P.corr_fixed + 65535LL * (1LL << 20);
     }
     uint64_t x = (uint64_t)t;
     x = (x & 0xffffffffu) + (x >> 32);
@@ -429,102 +402,108 @@ __device__ uint32_t finish_l4(const char* lds, uint32_t stash, const uint32_t* f
     return l4;
 }
 
-// Per-tile state of one wave. Every lane describes its GROUP's frame (the 4 lanes of a
-// group load the same descriptor; the group's lane 0 parses, finishes and stores it),
-// so no lane-to-lane broadcast is needed anywhere on the tile's critical path.
+// ---------------------------------------------------------------------------------------
+// Tile state. Every lane describes its GROUP's frame (the 4 lanes of a group load the same
+// descriptor; the group's lane 0 parses, finishes and stores it).
 struct Tile {
-    bool fvalid;
-    uint32_t fi, len, nd, ndall, sa, te;
-    uint64_t E, sdw;
-    // row/header load addressing: the group's own frame, or for an empty group (no frame, or
-    // a frame under 4 bytes, whose streams are never used) a longest frame of the tile, so
-    // that every load -- including the unclamped fast-path refills -- stays inside a frame
-    uint64_t ld_sdw;
-    int ld_nd, ld_ndall;
-    int R, Rp, rel0, lo;
-    int Rh;            // wave-uniform: last row holding header dwords [0, kHdrDwords) of any frame
-    int RF_lo, RF_hi;  // wave-uniform rows where every lane takes the fast path
+    uint64_t S;     // frame offset
+    uint32_t len;   // frame length (0 for groups past the batch end)
+    // row addressing: the group's own frame, or for an empty group a longest frame of the
+    // tile, so that every row load -- including the unclamped lean refills -- stays inside a frame
     const uint32_t* gfb;
+    int rel0;   // frame dword of this lane's chunk in row 0
+    int lo;     // lowest frame dword a clamped row load may start at
+    int P;      // wave-uniform: rows of the tile (a multiple of kPrefetch; 0 = no rows)
+    int H;      // wave-uniform: leading rows that take the masked path
+    // derived per use (they would otherwise hold VGPRs across the row loop)
+    __device__ __forceinline__ uint32_t sa() const { return (uint32_t)S & 3u; }
+    __device__ __forceinline__ uint64_t sdw() const { return S >> 2; }
+    // dwords the frame touches (incl. frames under 4 bytes)
+    __device__ __forceinline__ int ndall() const { return (int)((sa() + len + 3u) >> 2); }
+    // stream dwords (0: empty group -- past the batch end, or a frame under 4 bytes)
+    __device__ __forceinline__ int nd() const { return len >= 4u ? ndall() : 0; }
+    __device__ __forceinline__ uint32_t te() const {
+        const uint32_t e = (sa() + len) & 3u;
+        return e ? e : 4u;
+    }
+    __device__ __forceinline__ uint32_t tail_mask() const {
+        const uint32_t t = te();
+        return t == 4u ? 0xffffffffu : ((1u << (8u * t)) - 1u);
+    }
 };
 
-__device__ __forceinline__ void tile_descriptors(Tile& T, uint32_t tile, uint32_t grp, uint32_t n,
+__device__ __forceinline__ void tile_descriptors(uint32_t tile, uint32_t grp, uint32_t n,
                                                  const uint64_t* __restrict__ offsets,
-                                                 const uint32_t* __restrict__ lengths, uint64_t& S) {
-    T.fi = tile * kFramesPerTile + grp;
-    T.fvalid = T.fi < n;
-    // groups past the batch end read the last frame's descriptor with length 0 (their loads
-    // then use a longest frame of the tile, see tile_geometry; `frames` itself may lie
-    // outside the allocation: the host-staged path passes staging - first offset)
-    const uint32_t fl = T.fvalid ? T.fi : n - 1u;
-    // Inline asm: hipcc otherwise sinks the loads into their first use (past the region-A
-    // build and the tile branch), serializing two HBM round trips. The values are tied to
-    // an explicit wait (descriptors_ready) before use.
+                                                 const uint32_t* __restrict__ lengths, uint64_t& S, uint32_t& len) {
+    const uint32_t fi = tile * kFramesPerTile + grp;
+    // groups past the batch end read the last frame's descriptor (their length is zeroed)
+    const uint32_t fl = fi < n ? fi : n - 1u;
+    // Inline asm: hipcc otherwise sinks the loads into their first use, serializing two HBM
+    // round trips. The values are tied to an explicit wait (descriptors_ready) before use.
     asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(S) : "v"(offsets + fl));
-    asm volatile("global_load_dword %0, %1, off" : "=v"(T.len) : "v"(lengths + fl));
+    asm volatile("global_load_dword %0, %1, off" : "=v"(len) : "v"(lengths + fl));
 }
 
 // vmcnt(0) tied to the descriptor registers, so no use of them is scheduled above it.
-__device__ __forceinline__ void descriptors_ready(Tile& T, uint64_t& S) {
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(S), "+v"(T.len));
-    if (!T.fvalid) T.len = 0;
+__device__ __forceinline__ void descriptors_ready(uint64_t& S, uint32_t& len) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(S), "+v"(len));
 }
 
-// Wave max / min of a value that is uniform within each 4-lane group: two DPP row
-// mirrors combine the 4 groups of a 16-lane row, 4 readlanes the rows (no LDS permutes).
-template <bool kMax>
-__device__ __forceinline__ int group_reduce(int x) {
+// Wave max of a value that is uniform within each 4-lane group: two DPP row mirrors
+// combine the 4 groups of a 16-lane row, 4 readlanes the rows (no LDS permutes).
+__device__ __forceinline__ int group_max(int x) {
     int y = __builtin_amdgcn_mov_dpp(x, 0x140, 0xf, 0xf, false);  // row_mirror
-    x = kMax ? max(x, y) : min(x, y);
+    x = max(x, y);
     y = __builtin_amdgcn_mov_dpp(x, 0x141, 0xf, 0xf, false);      // row_half_mirror
-    x = kMax ? max(x, y) : min(x, y);
+    x = max(x, y);
     const int a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
     const int c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
-    return kMax ? max(max(a, b), max(c, d)) : min(min(a, b), min(c, d));
+    return max(max(a, b), max(c, d));
 }
 
-__device__ __forceinline__ void tile_geometry(Tile& T, uint64_t S, uint32_t gl, const uint8_t* __restrict__ frames) {
-    T.E = S + T.len;
-    T.sdw = S >> 2;
-    T.ndall = (uint32_t)(((T.E + 3u) >> 2) - T.sdw);
-    T.nd = (T.fvalid && T.len >= 4u) ? T.ndall : 0u;
-    T.sa = (uint32_t)(S & 3u);
-    T.te = (uint32_t)(T.E & 3u) ? (uint32_t)(T.E & 3u) : 4u;
-    const int nd = (int)T.nd;
+__device__ __forceinline__ void tile_geometry(Tile& T, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
+                                              uint64_t S, uint32_t len, const uint8_t* __restrict__ frames) {
+    T.len = (tile * kFramesPerTile + grp < n) ? len : 0u;
+    T.S = S;
+    const int nd = T.nd();
     const int rows = (nd + kRowDwords - 1) / kRowDwords;
-    T.R = group_reduce<true>(rows);
+    const int R = group_max(rows);
+    T.P = (R + kPrefetch - 1) / kPrefetch * kPrefetch;
+    uint64_t ld_sdw = T.sdw();
+    int ld_nd = nd;
     {
-        const uint64_t ball = __ballot(rows == T.R);  // never 0: some lane holds the maximum
+        const uint64_t ball = __ballot(rows == R);  // never 0: some lane holds the maximum
         const int src = (int)__builtin_ctzll(ball);
-        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)T.sdw, src);
-        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(T.sdw >> 32), src);
+        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ld_sdw, src);
+        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ld_sdw >> 32), src);
         const int s_nd = __builtin_amdgcn_readlane(nd, src);
-        const bool borrow = nd == 0;
-        T.ld_sdw = borrow ? (((uint64_t)s_hi << 32) | s_lo) : T.sdw;
-        T.ld_nd = borrow ? s_nd : nd;
-        T.ld_ndall = borrow ? s_nd : (int)T.ndall;
+        if (nd == 0) {
+            ld_sdw = ((uint64_t)s_hi << 32) | s_lo;
+            ld_nd = s_nd;
+        }
     }
-    // Rows padded at the FRONT to a multiple of kPrefetch: leading all-zero rows
-    // leave a zero-init CRC stream unchanged, so the loop needs no tail guard.
-    T.Rp = (T.R + kPrefetch - 1) / kPrefetch * kPrefetch;
-    T.gfb = reinterpret_cast<const uint32_t*>(frames + (T.ld_sdw << 2));
-    const int base0 = nd - kRowDwords * T.Rp;  // rel of the group's lane 0 in row 0
-    T.rel0 = T.ld_nd - kRowDwords * T.Rp + 4 * (int)gl;
-    T.Rh = group_reduce<true>(nd > 0 ? (kHdrDwords - 1 - base0) / kRowDwords : -1);
+    T.gfb = reinterpret_cast<const uint32_t*>(frames + (ld_sdw << 2));
+    T.rel0 = ld_nd - kRowDwords * T.P + 4 * (int)gl;
     // Loads of rows that start before the frame are clamped to the frame's first chunk (its last
     // chunk for frames under 4 dwords), so lanes idling through a tile's longest frame re-read
-    // one cached line instead of fetching the bytes that precede their frame; never below frames[0].
-    T.lo = max(T.ld_sdw > (1u << 24) ? -(1 << 24) : -(int)T.ld_sdw, min(0, T.ld_nd - 4));
-    // Fast rows: every lane's chunk [rel, rel+4) inside [kFastRel0, nd - 1) (no head/tail/init
-    // masks, whole chunk streamed into the checksum): lane 0 of the group bounds the start,
-    // lane 3 the end. Empty groups stream zeros and never force the slow path.
-    int flo = -0x40000000, fhi = 0x40000000;
-    if (nd > 0) {
-        const int a = kFastRel0 - base0, b = nd - 5 - (base0 + 12);  // rows r with a <= 16 r <= b
-        flo = (a <= 0) ? 0 : (a + kRowDwords - 1) / kRowDwords;
-        fhi = (b < 0) ? -1 : b / kRowDwords;
-    }
-    T.RF_lo = group_reduce<true>(flo);
-    T.RF_hi = group_reduce<false>(fhi);
+    // one cached line instead of fetching the bytes that precede their frame; a chunk that
+    // straddles the frame start is loaded where it lies unless that is below frames[0].
+    T.lo = max(ld_sdw > (1u << 24) ? -(1 << 24) : -(int)ld_sdw, min(0, ld_nd - 4));
+    // Masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
+    // dword before the frame. The group's lane 0 has the lowest rel: row r is lean for the
+    // group once nd - 16 P + 16 r >= 2.
+    const int need = 2 - (nd - kRowDwords * T.P);
+    const int h = (nd > 0 && need > 0) ? (need + kRowDwords - 1) / kRowDwords : 0;
+    T.H = min(group_max(h), T.P);
+}
+
+// Frame dword at which a masked row's chunk is loaded: where it lies, unless it starts
+// before the frame's first chunk (then the frame's first chunk: its dwords are all masked
+// or realigned) or below frames[0].
+__device__ __forceinline__ int load_pos(int rel, int lo) { return rel <= -4 ? lo : max(rel, lo); }
+
+__device__ __forceinline__ u32x4 load_row(const uint32_t* fb, int pos) {
+    return *reinterpret_cast<const u32x4_a4*>(fb + pos);
 }
 
 // Region A in place: thread t builds Z64[b][e] (b = t >> 8, e = t & 255) as the XOR of
@@ -552,28 +531,59 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
     dst[1] = u32x4{v, v, v, v};
 }
 
-// The plain tables by LDS-DMA: exactly kDmaPerWave 1-KB pieces per wave (surplus pieces
-// re-copy the last one with identical bytes). Inline asm, invisible to hipcc's vmcnt model
-// (the builtin makes it drain later LDS reads with vmcnt(0)); unknown VMEM ops only make
-// the compiler's own counted waits stricter. Waited for explicitly before the barrier.
-// (m0 is reserved to the compiler: this kernel sets it nowhere else, checked in the asm)
+// LDS-DMA by inline asm: invisible to hipcc's vmcnt model (the builtin makes it drain later
+// LDS reads with vmcnt(0)); unknown VMEM ops only make the compiler's own counted waits
+// stricter (loads retire in order). Every use is covered by an explicit counted wait.
+// (m0 is reserved to the compiler: it is written in the same statement that uses it)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, char* lds, uint32_t wave, uint32_t lane) {
-    typedef __attribute__((address_space(3))) char lds_char;
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)lds;
+__device__ __forceinline__ void dma_x4(const void* src, uint32_t lds_dst) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :
+                 : "v"(src), "s"(lds_dst)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ void dma_x1(const void* src, uint32_t lds_dst) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+                 :
+                 : "v"(src), "s"(lds_dst)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ uint32_t lds_base(const char* lds) {
+    typedef __attribute__((address_space(3))) const char lds_char;
+    return (uint32_t)(uintptr_t)(lds_char*)lds;
+}
+
+// The plain tables: exactly kDmaPerWave 1-KB pieces per wave (surplus pieces re-copy the
+// last one with identical bytes).
+__device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, const char* lds, uint32_t wave,
+                                          uint32_t lane) {
+    const uint32_t lds0 = lds_base(lds);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
     for (uint32_t k = 0; k < kDmaPerWave; ++k) {
         const uint32_t c = kPlainChunk0 + min(w0 + k * kWavesPerBlock, kPlainChunks - 1u);
-        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                     :
-                     : "v"(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u),
-                       "s"(__builtin_amdgcn_readfirstlane(lds0 + c * 1024u))
-                     : "memory", "m0");
+        dma_x4(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
+               __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
     }
 }
-#pragma clang diagnostic pop
+
+// The tile's header slots: 8 dword DMAs; instruction i writes frame dword x = 4i + gl of
+// every group (lane-linear: LDS byte hw + 256 i + 4 lane). Sources are clamped to the
+// frame's last dword (never past it).
+__device__ __forceinline__ void header_dma(const Tile& T, const uint8_t* __restrict__ frames, const char* lds,
+                                           uint32_t hw, uint32_t gl) {
+    const uint32_t hdr0 = __builtin_amdgcn_readfirstlane(lds_base(lds) + hw);
+    const int last = T.ndall() - 1;
+    const bool own = T.len > 0u;
+    const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2));
+    if (own) {  // exec-masked: a group with no frame bytes writes nothing (its slot is never used)
+#pragma unroll
+        for (int i = 0; i < kHdrDmas; ++i) dma_x1(fbs + min(4 * i + (int)gl, last), hdr0 + 256u * i);
+    }
+}
 
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
@@ -588,11 +598,8 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     const uint32_t gwave = blockIdx.x * kWavesPerBlock + wave;
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
     const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
-    const uint32_t hdr_wave = kLdsHdr + wave * kHdrWaveBytes;
-    const uint32_t stash_base = kLdsStash + wave * (kFramesPerTile * kStashBytes);
+    const uint32_t hw = kLdsHdr + wave * kHdrWaveBytes;  // this wave's header slots
 
-    const uint32_t hb = hdr_wave + kHdrSlotBytes * grp;         // the group's header slot
-    const uint32_t stash = stash_base + grp * kStashBytes;      // the group's last-row stash
     LaneKeys keys;
     {
         const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
@@ -606,90 +613,94 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         }
     }
 
-    // Preamble: the first tile's descriptors (one round trip), its geometry, the row
-    // prefetch, and only THEN the table LDS-DMA, so that the CU's in-order vector-memory
-    // queue serves the descriptors and the first rows before the 100 KB of table pieces;
-    // the DMA (L2 hits) then overlaps the rows' HBM latency. hipcc does not count LDS-DMA
-    // in its vmcnt model: the DMA is issued last and drained with an explicit vmcnt(0),
-    // which the first row needs anyway.
     // Preamble: the first tile's descriptors (the first memory ops, one round trip) while
     // region A is built in place by VALU; geometry; the plain tables' LDS-DMA (36 KB, L2
-    // hits); the row prefetch; one barrier once this wave's table pieces have landed.
+    // hits); the header DMA; the row prefetch; one barrier once this wave's table pieces
+    // have landed.
     uint32_t tile = gwave;
     FS_RTSTAMP(5);
     FS_STAMP(0);
     Tile T;
-    uint64_t S;
     u32x4 pf[kPrefetch];
-    tile_descriptors(T, tile, grp, n, offsets, lengths, S);
-    build_region_a(tabs, lds);
-    descriptors_ready(T, S);
-#if defined(FS_STAMPS) && FS_STAMPS == 2
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // fine-stamp build only: time the descriptor round trip
-    FS_STAMP(8);
-#endif
-    bool rows0 = false;  // the first tile has rows (and so a row prefetch in flight)
-    if (__builtin_amdgcn_readfirstlane(tile) < ntiles) {
-        tile_geometry(T, S, gl, frames);
-        rows0 = T.Rp > 0;
+    const bool first = __builtin_amdgcn_readfirstlane(tile) < ntiles;
+    {
+        uint64_t S;
+        uint32_t len;
+        tile_descriptors(tile, grp, n, offsets, lengths, S, len);
+        build_region_a(tabs, lds);
+        descriptors_ready(S, len);
+        T.P = 0;
+        if (first) tile_geometry(T, tile, grp, gl, n, S, len, frames);
     }
     plain_dma(tabs, lds, wave, lane);
-    if (rows0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
+    if (first) {
+        header_dma(T, frames, lds, hw, gl);
+        if (T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-        for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
+            for (int i = 0; i < kPrefetch; ++i) {
+                const int rel = T.rel0 + kRowDwords * i;
+                pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
+            }
+        }
     }
     FS_STAMP(9);
-    // the table pieces are older than the rows: vmcnt(kPrefetch) (vmcnt(0) without rows);
+    // the table pieces are older than the header DMA and the rows: vmcnt(header + rows);
     // lgkmcnt(0): this wave's region-A stores
     // s_waitcnt field layout (gfx9): vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4], lgkmcnt[11:8]
-    if (rows0) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
+    if (first && T.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | (kPrefetch + kHdrDmas));
+    else if (first) __builtin_amdgcn_s_waitcnt(0x0070 | kHdrDmas);
     else __builtin_amdgcn_s_waitcnt(0x0070);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     FS_STAMP(1);
 
     while (tile < ntiles) {
-        RowMasks M;
-        M.nd = (int)T.nd;
-        M.head_mask = 0xffffffffu << (8u * T.sa);
-        M.init1 = (1u << (8u * T.sa)) - 1u;
-        M.tail_mask = (T.te == 4u) ? 0xffffffffu : ((1u << (8u * T.te)) - 1u);
 
-        // ---- main loop: rows 0..Rp-1 in blocks of kPrefetch rows with kPrefetch rows in
-        // flight; the last block does not refill (nothing lies past the frame end). Blocks
-        // whose rows are all fast for every lane run the lean path: four Z64 steps + four
-        // v_sad_u16 per row and a refill with an immediate row offset.
         uint32_t A[4] = {0u, 0u, 0u, 0u};
         uint32_t cs = 0u;
-        const bool parser = T.fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
-        // the header parse runs once the block holding row Rh (the last row with header dwords)
-        // has been captured, while the ring's loads are in flight
-        const uint64_t fS = T.E - T.len;
-        const uint32_t fsa = T.sa, flen = T.len;
-        auto parse = [&]() {
-            if (parser) park_parsed(lds, hb, parse_frame(lds, hb, fsa, flen, mtu), fS, flen);
+        const bool fvalid = tile * kFramesPerTile + grp < n;
+        const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
+
+        // ---- header parse: after the first block of rows, while the ring's loads are in flight.
+        // The header DMA was issued before the tile's rows; vmcnt(kPrefetch) retires it once the
+        // first block's refills are the only younger loads.
+        auto parse = [&](bool refilled) {
+            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
+            else __builtin_amdgcn_s_waitcnt(0x0070);
+            // group-vectorised sums over the slot (all lanes of valid groups take part)
+            const uint32_t sa = T.sa(), len = T.len;
+            const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2));
+            const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3));
+            const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
+            const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 4)) >> 16;
+            const uint32_t end = (14u + tl) & 0xffffu;
+            // [0, off) spans at most 3 + 74 bytes: absolute dwords < 20
+            const uint32_t hsum = slot_sum(lds, hw, grp, gl, sa, 0, (int)min(off, len), 5);
+            const bool pad_in_slot = sa + len <= 4u * kHdrDwords;
+            int64_t pad = -1;
+            if (__ballot(len >= 34u && end < len && pad_in_slot) != 0) {
+                const uint32_t ps = slot_sum(lds, hw, grp, gl, sa, (int)min(end, len), (int)len, kHdrDwords / 4);
+                if (pad_in_slot) pad = (int64_t)ps;
+            }
+#ifndef FS_NOPARSE
+            if (parser) park_parsed(lds, hw, grp, parse_frame(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
+#else
+            if (parser) *reinterpret_cast<uint32_t*>(lds + hdr_at(hw, grp, 0)) = hsum + (uint32_t)pad;
+#endif
         };
         auto prio = [&](int r0) {
             // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
             // a wave with more rows left gets a higher priority.
-            if (FS_PRIO == 2) {
-                // static, inverted age rank: the SIMD arbiter favours older waves on ties, so
-                // the younger waves (higher wave index) get the higher priority
-                const uint32_t rank = __builtin_amdgcn_readfirstlane(wave) >> 2;
-                if (rank == 3) __builtin_amdgcn_s_setprio(3);
-                else if (rank == 2) __builtin_amdgcn_s_setprio(2);
-                else if (rank == 1) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            } else if (FS_PRIO) {
-                const int left4 = (4 * (T.Rp - r0)) / max(T.Rp, 1);  // 4 .. 1
+            if (FS_PRIO) {
+                const int left4 = (4 * (T.P - r0)) / max(T.P, 1);  // 4 .. 1
                 if (left4 >= 4) __builtin_amdgcn_s_setprio(3);
                 else if (left4 == 3) __builtin_amdgcn_s_setprio(2);
                 else if (left4 == 2) __builtin_amdgcn_s_setprio(1);
                 else __builtin_amdgcn_s_setprio(0);
             }
         };
-        // general block: per-row fast/slow (scalar), header capture for rows <= Rh (scalar),
-        // clamped refill addresses
+        // general block: rows below H take the masked path (scalar branch per row); refills
+        // of rows below H are clamped
         auto block = [&](int r0, auto refill_tag) {
             constexpr bool kRefill = decltype(refill_tag)::value;
             prio(r0);
@@ -697,24 +708,26 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
             for (int i = 0; i < kPrefetch; ++i) {
                 const int r = r0 + i;
                 const int rel = T.rel0 + kRowDwords * r;
-                const bool fast = (r >= T.RF_lo) && (r <= T.RF_hi);  // wave-uniform (scalar)
-                if (r <= T.Rh) capture_header(lds, hb, rel, T.lo, pf[i]);
                 // consume the ring slot, then refill the SAME registers: no copy of an
                 // in-flight load, so the compiler keeps kPrefetch-1 loads outstanding
-                process_row(lds, keys, pf[i], rel, fast, M, T.lo, A, cs);
-                if (kRefill && FS_DIAG != 3) pf[i] = load_chunk(T.gfb, rel + kRowDwords * kPrefetch, T.lo);
+                if (r < T.H) masked_row(lds, keys, pf[i], rel, load_pos(rel, T.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
+                else lean_row(lds, keys, pf[i], A, cs);
+                if (kRefill) {
+                    const int rn = rel + kRowDwords * kPrefetch;
+                    pf[i] = load_row(T.gfb, r + kPrefetch < T.H ? load_pos(rn, T.lo) : rn);
+                }
             }
         };
-        // lean block: every row fast for every lane; the refills of a fast row's successors
-        // lie inside the frame, so they need no clamp: one pointer per block, immediate
-        // row offsets
-        auto lean_block = [&](int r0) {
+        // lean block: every row lean for every lane; the refills lie inside the frame, so they
+        // need no clamp: one pointer per block, immediate row offsets
+        auto lean_block = [&](int r0, auto refill_tag) {
+            constexpr bool kRefill = decltype(refill_tag)::value;
             prio(r0);
             const uint32_t* pb = T.gfb + (T.rel0 + kRowDwords * (r0 + kPrefetch));
 #pragma unroll
             for (int i = 0; i < kPrefetch; ++i) {
-                process_row(lds, keys, pf[i], 0, true, M, 0, A, cs);
-                if (FS_DIAG != 3) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
+                lean_row(lds, keys, pf[i], A, cs);
+                if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
                 // keep consume/refill interleaved per row: unfenced, the scheduler sinks all
                 // refills to the block end behind a vmcnt(0), draining the ring every block
                 __builtin_amdgcn_sched_barrier(0);
@@ -722,79 +735,87 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         };
         using Yes = std::true_type;
         using No = std::false_type;
-        const int Rc = T.Rp - kPrefetch;
-        if (T.Rp > 0) {
-            // blocks: [head: general] [body: lean] [tail: general] [last: general, no refill],
-            // as three loops in sequence (one code path per loop keeps the ring registers fixed)
-            // (a block is lean only past Rh, so the header rows are always in general blocks)
-            int r0 = 0;
-            for (; r0 < Rc && !(r0 > T.Rh && r0 >= T.RF_lo && r0 + kPrefetch - 1 <= T.RF_hi); r0 += kPrefetch) {
-                block(r0, Yes());
-                if (T.Rh >= r0 && T.Rh < r0 + kPrefetch) parse();
+        const int Rc = T.P - kPrefetch;  // first row of the last block
+        if (T.P > 0) {
+            // [first block] parse [head blocks: general] [body: lean] [last block: no refill]
+            if (Rc > 0) {
+                if (T.H > 0) block(0, Yes());
+                else lean_block(0, Yes());
+                parse(true);
+                int r0 = kPrefetch;
+                for (; r0 < Rc && r0 < T.H; r0 += kPrefetch) block(r0, Yes());
+                for (; r0 < Rc; r0 += kPrefetch) lean_block(r0, Yes());
+                if (Rc < T.H) block(Rc, No());
+                else lean_block(Rc, No());
+            } else {
+                if (T.H > 0) block(0, No());
+                else lean_block(0, No());
+                parse(false);
             }
-            for (; r0 < Rc && r0 + kPrefetch - 1 <= T.RF_hi; r0 += kPrefetch) lean_block(r0);
-            for (; r0 < Rc; r0 += kPrefetch) block(r0, Yes());
-            block(Rc, No());
-            if (T.Rh >= Rc) parse();
         } else {
-            parse();  // no rows (every frame of the tile under 4 bytes): rejected by length
+            parse(false);  // no rows (every frame of the tile under 4 bytes): rejected by length
         }
         FS_STAMP(2);
-        // the last ring slot holds the frame's final row: stash it for the padding sum
-        *reinterpret_cast<u32x4*>(lds + stash + 16u * gl) = pf[kPrefetch - 1];
 
         // ---- combine the 16 streams of each frame: C = Z_(4-t)( xor_l Z_16(3-l)( U_l ) ),
         //      U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3   (3 dependent LDS round trips).
-        const uint32_t U = zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3];
+        // The last row was lean (unless every row was masked): its last dword -- lane 3's
+        // 4th -- still holds the up to 3 bytes past the frame end. Their CRC contribution is
+        // that junk itself (the last dword enters the combine unshifted) and their sum is
+        // sad16 of it: remove both.
+        uint32_t junk = 0u;
+        if (T.P > 0 && T.H < T.P && gl == 3u && T.nd() > 0) junk = pf[kPrefetch - 1].w & ~T.tail_mask();
+        const uint32_t U =
+            zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3] ^ junk;
+        cs -= sad16(junk, 0u);
         const uint32_t ybase = (gl == 0u) ? kLdsZ48 : (gl == 1u) ? kLdsZ32 : kLdsZ16;
         uint32_t Y = zplain(lds, U, ybase);
         if (gl == 3u) Y = U;
         Y ^= dpp_quad<kQuadXor1>(Y);
         Y ^= dpp_quad<kQuadXor2>(Y);
-        // checksum partial sum over the 4 lanes of the group (each < 2^30: no u32 overflow)
+        // checksum over the 4 lanes of the group, each lane first folded mod 65535 (the finish
+        // only needs the total mod 65535; the fold keeps every partial < 2^18)
+        cs = (cs & 0xffffu) + (cs >> 16);
         cs += dpp_quad<kQuadXor1>(cs);
         cs += dpp_quad<kQuadXor2>(cs);
-        const uint64_t csum = cs;
-
         FS_STAMP(3);
-        // ---- the group's lane 0: finish and store (its frame's state comes back from LDS).
+        // ---- the group's lane 0: finish and store (its frame's parse comes back from LDS).
         if (parser) {
-            uint64_t fS;
-            uint32_t flen;
-            const Parsed P = unpark_parsed(lds, hb, fS, flen);
-            const uint64_t fE = fS + flen, fsdw = fS >> 2;
-            const uint32_t fsa = (uint32_t)(fS & 3u), fte = (uint32_t)(fE & 3u) ? (uint32_t)(fE & 3u) : 4u;
-            const uint32_t fnd = flen >= 4u ? (uint32_t)(((fE + 3u) >> 2) - fsdw) : 0u;
-            const uint32_t fi = tile * kFramesPerTile + grp;
+            const Parsed P = unpark_parsed(lds, hw, grp);
             uint32_t crcv;
-            if (flen < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
+            const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2));
+            if (T.len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
                 uint32_t c = 0xffffffffu;
-                const uint8_t* fbytes = frames + fS;
-                for (uint32_t p = 0; p < flen; ++p)
+                const uint8_t* fbytes = frames + T.S;
+                for (uint32_t p = 0; p < T.len; ++p)
                     c = lds32(lds, kLdsZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
                 crcv = ~c;
             } else {
-                const uint32_t tpad = (4u - fte) & 3u;  // zero bytes appended by the dword rounding
+                const uint32_t tpad = (4u - T.te()) & 3u;  // zero bytes appended by the dword rounding
                 crcv = ~zplain(lds, Y, kLdsZfin + 4096u * tpad);
             }
             uint32_t verdict = P.verdict, l4 = 0u;
-            if (P.compute) {
-                const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + fsdw * 4u);
-                l4 = finish_l4(lds, stash, fb, fsa, flen, fnd, P, csum, verdict);
-            }
+            if (P.compute) l4 = finish_l4(fbs, T.sa(), T.len, P, cs, verdict);
+            const uint32_t fi = tile * kFramesPerTile + grp;
             out[fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
             if (status) status[fi] = (uint8_t)verdict;
         }
         FS_STAMP(4);
         FS_RTSTAMP(6);
         tile += nwaves;
-        if (tile < ntiles) {  // next tile: descriptors, geometry, row prefetch
-            tile_descriptors(T, tile, grp, n, offsets, lengths, S);
-            descriptors_ready(T, S);
-            tile_geometry(T, S, gl, frames);
-            if (T.Rp > 0) {
+        if (tile < ntiles) {  // next tile: descriptors, geometry, header DMA, row prefetch
+            uint64_t S;
+            uint32_t len;
+            tile_descriptors(tile, grp, n, offsets, lengths, S, len);
+            descriptors_ready(S, len);
+            tile_geometry(T, tile, grp, gl, n, S, len, frames);
+            header_dma(T, frames, lds, hw, gl);
+            if (T.P > 0) {
 #pragma unroll
-                for (int i = 0; i < kPrefetch; ++i) pf[i] = load_chunk(T.gfb, T.rel0 + kRowDwords * i, T.lo);
+                for (int i = 0; i < kPrefetch; ++i) {
+                    const int rel = T.rel0 + kRowDwords * i;
+                    pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
+                }
             }
         }
     }

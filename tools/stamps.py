@@ -62,3 +62,11 @@ if s[:, 9].any():
         if s[:, b_].any() and s[:, a_].any():
             d = s[:, b_] - s[:, a_]
             print(f"  {nm:18s} median {int(np.median(d)):8d}  p10 {int(np.percentile(d, 10)):8d}  p90 {int(np.percentile(d, 90)):8d}")
+# active-wave profile over the launch (realtime, 1-us bins) and the phase boundaries' spread
+span = us(re_.max() - t0)
+bins = np.arange(0, span + 1.0, 1.0)
+act = [int(((us(rs - t0) <= b + 0.5) & (us(re_ - t0) > b + 0.5)).sum()) for b in bins]
+print("  active waves per 1-us bin:", act)
+ends = np.sort(us(re_ - t0))
+print("  wave end quantiles (us) 1/5/25/50/75/95/99/100%:",
+      [round(float(np.percentile(ends, q)), 2) for q in (1, 5, 25, 50, 75, 95, 99, 100)])
