@@ -691,7 +691,7 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         auto prio = [&](int r0) {
             // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
             // a wave with more rows left gets a higher priority.
-            if (FS_PRIO) {
+            if (FS_PRIO && T.P > 36) {  // long tiles only (C2-size tiles run faster without)
                 const int left4 = (4 * (T.P - r0)) / max(T.P, 1);  // 4 .. 1
                 if (left4 >= 4) __builtin_amdgcn_s_setprio(3);
                 else if (left4 == 3) __builtin_amdgcn_s_setprio(2);
