@@ -98,7 +98,8 @@ const char* fs_last_error(const fs_ctx* ctx);
 /* Batched digest, device-resident. All pointers are DEVICE pointers.
  *   frame i = frames[offsets[i] : offsets[i] + lengths[i]]  (any byte alignment,
  *   frames may overlap or be sparse; the engine may read up to 3 bytes past a
- *   frame's end, i.e. `frames` must be readable up to round_up(end, 4)).
+ *   frame's end, i.e. `frames` must be readable up to round_up(end, 4), and up
+ *   to 12 bytes before a frame's start, but never before frames[0]).
  *   out[i] receives the digest; status (nullable) receives the fs_verdict.
  * Asynchronous on `stream` (a hipStream_t; NULL = the null stream). */
 fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths,
@@ -110,6 +111,14 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
  * (fs_host_alloc) gives full PCIe rate; pageable memory works. */
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status);
+
+/* Kernel variant of a context's launches. The engine has two: a one-pass kernel
+ * for batches of similar frame lengths, and one that splits long frames into
+ * 768-byte pieces when a tile of 16 frames mixes very different lengths. By
+ * default (variant 0) every launch reports whether its batch had such tiles and
+ * the next launch picks accordingly. 1 forces the one-pass kernel, 2 the mixed
+ * one. Results are identical in every case; only the speed differs. */
+fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
 /* Pinned host memory helpers for fs_digest_batch_host callers. */
 fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out);

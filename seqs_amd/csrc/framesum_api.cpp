@@ -39,6 +39,10 @@ struct fs_ctx {
     int device = 0;
     int num_cus = 0;
     FsTables* d_tables = nullptr;
+    // host-mapped word the kernels set when a batch has widely mixed lengths (launch_digest)
+    volatile uint32_t* h_report = nullptr;
+    uint32_t* d_report = nullptr;
+    int force_kernel = 0;  // fs_ctx_set_kernel
     HostSlot slot[kHostSlots];
     hipStream_t copy_stream = nullptr, compute_stream = nullptr;
     // pinned host mirrors of the descriptors and results, so every per-chunk copy is
@@ -148,6 +152,15 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
     framesum::build_tables(h);
     e = hipMalloc(&ctx->d_tables, sizeof(FsTables));
     if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, h, sizeof(FsTables), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        void* hp = nullptr;
+        e = hipHostMalloc(&hp, 64, hipHostMallocMapped);
+        if (e == hipSuccess) {
+            ctx->h_report = static_cast<volatile uint32_t*>(hp);
+            *ctx->h_report = 0u;
+            e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_report), hp, 0);
+        }
+    }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->compute_stream, hipStreamNonBlocking);
     for (int k = 0; k < kHostSlots && e == hipSuccess; ++k) {
@@ -181,6 +194,7 @@ fs_status fs_ctx_destroy(fs_ctx* ctx) {
         (void)hipFree(sl.d_status);
     }
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+    if (ctx->h_report) (void)hipHostFree(const_cast<uint32_t*>(ctx->h_report));
     (void)hipFree(ctx->d_tables);
     delete ctx;
     return FS_SUCCESS;
@@ -197,7 +211,8 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch: frames must be 4-byte aligned");
     FS_HIP(ctx, hipSetDevice(ctx->device));
     FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
-                                        reinterpret_cast<hipStream_t>(stream), ctx->num_cus));
+                                        reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
+                                        ctx->d_report, ctx->force_kernel));
     return FS_SUCCESS;
 }
 
@@ -262,7 +277,8 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         // the kernel addresses frame i at base + offsets[i]: base = staging - cpy_lo (4-B aligned)
         const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
         FS_HIP(ctx, framesum::launch_digest(base, sl.d_offsets, sl.d_lengths, cnt, mtu, ctx->d_tables, sl.d_out,
-                                            status ? sl.d_status : nullptr, ks, ctx->num_cus));
+                                            status ? sl.d_status : nullptr, ks, ctx->num_cus, ctx->h_report,
+                                            ctx->d_report, ctx->force_kernel));
         FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
         sl.used = true;
         FS_HIP(ctx, hipMemcpyAsync(h_out + c0, sl.d_out, (size_t)cnt * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
@@ -272,6 +288,13 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));
     std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
     if (status) std::memcpy(status, h_st, n);
+    return FS_SUCCESS;
+}
+
+fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
+    if (!ctx) return FS_E_INVALID;
+    if (variant < 0 || variant > 2) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0, 1 or 2");
+    ctx->force_kernel = variant;
     return FS_SUCCESS;
 }
 

@@ -26,17 +26,23 @@ struct FsTables {
     uint32_t z48[4][256];      // Z_48 : lane 0 of the flattened lane tree
     uint32_t z12[4][256];      // Z_12 : stream 0 of the flattened intra-lane combine
     uint32_t z8[4][256];       // Z_8  : stream 1
+    uint32_t z768[4][256];     // Z_768: one full piece (mode B Horner over a frame's pieces)
     // --- not part of the LDS image ---
     uint32_t z64_basis[4][8];  // Z_64[b][1 << j]: region A's entries are XORs of these
 };
-constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 9;  // the LDS image: everything before z64_basis
+constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 10;  // the LDS image: everything before z64_basis
 static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout");
 
 void build_tables(FsTables* t);
 
-// Launch the digest kernel. `num_cus` sizes the persistent grid.
+// Launch the digest kernel. `num_cus` sizes the persistent grid. `report` (nullable) is a
+// host-mapped word: a kernel writes its launch id there when its batch has tiles of widely
+// mixed frame lengths; launches within a window after such a report use the kernel variant
+// that can split long frames into pieces (mode B), others the leaner one-pass variant. The choice never changes a
+// result, only the speed. `force`: 0 = that choice, 1 = always the one-pass kernel, 2 = always
+// the mixed-length kernel (fs_ctx_set_kernel; tests run every case through both).
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
-                         int num_cus);
+                         int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force = 0);
 
 }  // namespace framesum

@@ -43,6 +43,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <type_traits>
 
 #include "framesum_internal.h"
@@ -83,14 +84,27 @@ constexpr uint32_t kLdsZfin = kLdsZ16 + 4096;  // Z4, Z3, Z2, Z1 (4 KB each)
 constexpr uint32_t kLdsZ48 = kLdsZfin + 16384;
 constexpr uint32_t kLdsZ12 = kLdsZ48 + 4096;
 constexpr uint32_t kLdsZ8 = kLdsZ12 + 4096;
-constexpr uint32_t kLdsTables = kLdsZ8 + 4096;
+constexpr uint32_t kLdsZ768 = kLdsZ8 + 4096;    // Z_768: shift past one full piece (mode B)
+constexpr uint32_t kLdsTables = kLdsZ768 + 4096;
 constexpr uint32_t kLdsHdr = kLdsTables;
-constexpr uint32_t kLdsBytes = kLdsHdr + kWavesPerBlock * kHdrWaveBytes;
+// mode B pieces (see "Tiles, pieces and passes")
+constexpr int kPieceRows = 12;
+constexpr int kPieceDwords = kPieceRows * kRowDwords;  // 192 dwords = 768 bytes
+constexpr int kMaxFullPasses = 6;
+constexpr uint32_t kWaveScratchBytes = 16u * kFramesPerTile + 8u * kFramesPerTile +
+                                       8u * (kFramesPerTile + kFramesPerTile * kMaxFullPasses);
+constexpr uint32_t kLdsWave = kLdsHdr + kWavesPerBlock * kHdrWaveBytes;
+constexpr uint32_t kLdsBytes = kLdsWave + kWavesPerBlock * kWaveScratchBytes;
+static_assert(kPieceRows % kPrefetch == 0, "a piece is whole blocks of rows");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kTablesLdsBytes == kLdsTables, "FsTables is the LDS image of the tables");
 constexpr uint32_t kPlainChunk0 = 65536 / 1024;                     // first 1-KB piece of the plain tables
-constexpr uint32_t kPlainChunks = (kLdsTables - 65536) / 1024;      // 36 pieces
+constexpr uint32_t kPlainChunks = (kLdsTables - 65536) / 1024;      // 40 pieces
 constexpr uint32_t kDmaPerWave = (kPlainChunks + kWavesPerBlock - 1) / kWavesPerBlock;
+
+// The workgroup's LDS image (static allocation of digest_kernel). Namespace scope, so the
+// out-of-line parse routine addresses it as LDS (ds_read), not through a flat pointer.
+__shared__ __attribute__((aligned(16))) char g_lds[kLdsBytes];
 
 #ifdef FS_STAMPS
 // Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
@@ -274,7 +288,7 @@ struct Parsed {
 // compare the two). Reads only the LDS header slot; `hsum` = sum of frame bytes [0, off)
 // and `pad` = sum of the Ethernet padding [end, len), both from the group-vectorised sums
 // (pad < 0: the padding lies past the slot, summed here from global memory).
-__device__ __attribute__((noinline)) Parsed parse_frame(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t len, uint32_t mtu,
+__device__ __forceinline__ Parsed parse_frame(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t len, uint32_t mtu,
                               uint32_t hsum, int64_t pad, const uint32_t* fb) {
     Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0};
     if (len < 34u) { r.verdict = V_SMOL; return r; }                          // portstack.go:167-168
@@ -381,6 +395,29 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, ui
     return P;
 }
 
+// The whole header parse of a tile, out of line so that its registers are allocated apart
+// from the row loop's (it needs fewer than the 40 VGPRs below the callee-saved range, so the
+// call saves nothing). Every lane takes part: group-vectorised sums over the header slot
+// (the bytes [0, off) of the Ethernet + IP headers; the Ethernet padding [end, len) when it
+// lies in the slot), then the parser lane's gates and corrections, parked in LDS.
+__device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
+                                                     uint32_t mtu, const uint32_t* fbs, bool parser) {
+    const char* lds = g_lds;
+    const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3));
+    const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
+    const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 4)) >> 16;
+    const uint32_t end = (14u + tl) & 0xffffu;
+    // [0, off) spans at most 3 + 74 bytes: absolute dwords < 20
+    const uint32_t hsum = slot_sum(lds, hw, grp, gl, sa, 0, (int)min(off, len), 5);
+    const bool pad_in_slot = sa + len <= 4u * kHdrDwords;
+    int64_t pad = -1;
+    if (__ballot(len >= 34u && end < len && pad_in_slot) != 0) {
+        const uint32_t ps = slot_sum(lds, hw, grp, gl, sa, (int)min(end, len), (int)len, kHdrDwords / 4);
+        if (pad_in_slot) pad = (int64_t)ps;
+    }
+    if (parser) park_parsed(g_lds, hw, grp, parse_frame(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
+}
+
 // Final L4 checksum + verdict (parser lane) once the streamed sum is known.
 __device__ uint32_t finish_l4(const uint32_t* fb, uint32_t sa, uint32_t len, const Parsed& P, uint64_t main_sum,
                               uint32_t& verdict) {
@@ -403,9 +440,222 @@ __device__ uint32_t finish_l4(const uint32_t* fb, uint32_t sa, uint32_t len, con
 }
 
 // ---------------------------------------------------------------------------------------
-// Tile state. Every lane describes its GROUP's frame (the 4 lanes of a group load the same
-// descriptor; the group's lane 0 parses, finishes and stores it).
+// Tiles, pieces and passes.
+//
+// A tile's 16 frames run in PASSES of lockstep rows. MODE A (one pass): every group streams
+// its whole frame, rows end-anchored at the pass end -- the lean choice when the frames have
+// similar lengths. MODE B, for tiles whose lengths differ widely: a frame of nd stream dwords
+// is cut into a HEAD piece of nd0 = nd - 192 (npc - 1) dwords (2 <= nd0 <= 193) and npc - 1
+// FULL pieces of 192 dwords (12 rows, kPieceRows) that follow it; pass 0 streams every
+// group's head piece exactly as mode A streams whole frames; passes 1.. stream the tile's F
+// full pieces, 16 per pass (full piece q -> group q mod 16 of pass 1 + q / 16), all lean.
+// Each pass ends with the 16-stream combine of every group's piece into one register value
+// Y and a checksum partial, parked in a per-wave LDS slot; a frame's CRC register is then
+// the Horner fold C = Z768(C) ^ Y over its pieces (a piece's value is its contribution as
+// if the frame ended with it; Z768 shifts it past one full piece). Every pass runs the same
+// row loop; the next pass's first rows are prefetched before the current pass's combine.
+
+// The group's own frame (parse and finish). Every lane describes its GROUP's frame (the 4
+// lanes of a group load the same descriptor; the group's lane 0 parses, finishes and stores).
 struct Tile {
+    uint64_t S;     // frame offset
+    uint32_t len;   // frame length (0 for groups past the batch end)
+    int npass;      // wave-uniform: 1 (mode A) or 1 + ceil(F / 16) (mode B)
+    int F;          // wave-uniform: full pieces of the tile (mode B)
+    __device__ __forceinline__ uint32_t sa() const { return (uint32_t)S & 3u; }
+    __device__ __forceinline__ uint64_t sdw() const { return S >> 2; }
+    // dwords the frame touches (incl. frames under 4 bytes)
+    __device__ __forceinline__ int ndall() const { return (int)((sa() + len + 3u) >> 2); }
+    // stream dwords (0: empty group -- past the batch end, or a frame under 4 bytes)
+    __device__ __forceinline__ int nd() const { return len >= 4u ? ndall() : 0; }
+    __device__ __forceinline__ uint32_t te() const {
+        const uint32_t e = (sa() + len) & 3u;
+        return e ? e : 4u;
+    }
+    __device__ __forceinline__ uint32_t tail_mask() const {
+        const uint32_t t = te();
+        return t == 4u ? 0xffffffffu : ((1u << (8u * t)) - 1u);
+    }
+};
+
+__device__ __forceinline__ int pieces_of(int nd) { return nd <= 1 ? 1 : (nd - 1 + kPieceDwords - 1) / kPieceDwords; }
+
+// The rows one pass streams.
+struct Unit {
+    const uint32_t* gfb;  // frame dword 0 of the lane's rows (a longest frame's for an empty group)
+    int rel0;   // frame dword of this lane's chunk in row 0
+    int lo;     // lowest frame dword a clamped row load may start at
+    int P;      // wave-uniform: rows (a multiple of kPrefetch; 0 = no rows)
+    int H;      // wave-uniform: leading rows that take the masked path
+    // mode B: bit 31 valid piece, bit 30 the frame's last piece (its last dword carries the
+    // dword-rounding junk), bits 28-29 the frame's end byte in its last dword, bits 0-15 slot
+    uint32_t info;
+};
+
+__device__ __forceinline__ void tile_descriptors(uint32_t tile, uint32_t grp, uint32_t n,
+                                                 const uint64_t* __restrict__ offsets,
+                                                 const uint32_t* __restrict__ lengths, uint64_t& S, uint32_t& len) {
+    const uint32_t fi = tile * kFramesPerTile + grp;
+    // groups past the batch end read the last frame's descriptor (their length is zeroed)
+    const uint32_t fl = fi < n ? fi : n - 1u;
+    // Inline asm: hipcc otherwise sinks the loads into their first use, serializing two HBM
+    // round trips. The values are tied to an explicit wait (descriptors_ready) before use.
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(S) : "v"(offsets + fl));
+    asm volatile("global_load_dword %0, %1, off" : "=v"(len) : "v"(lengths + fl));
+}
+
+// vmcnt(0) tied to the descriptor registers, so no use of them is scheduled above it.
+__device__ __forceinline__ void descriptors_ready(uint64_t& S, uint32_t& len) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(S), "+v"(len));
+}
+
+// Wave max (sum) of a value that is uniform within each 4-lane group: two DPP row mirrors
+// combine the 4 groups of a 16-lane row, 4 readlanes the rows (no LDS permutes).
+__device__ __forceinline__ int group_max(int x) {
+    int y = __builtin_amdgcn_mov_dpp(x, 0x140, 0xf, 0xf, false);  // row_mirror
+    x = max(x, y);
+    y = __builtin_amdgcn_mov_dpp(x, 0x141, 0xf, 0xf, false);      // row_half_mirror
+    x = max(x, y);
+    const int a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
+    const int c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
+    return max(max(a, b), max(c, d));
+}
+__device__ __forceinline__ int group_sum(int x) {
+    x += __builtin_amdgcn_mov_dpp(x, 0x140, 0xf, 0xf, false);  // lane i + lane 15-i: two groups
+    x += __builtin_amdgcn_mov_dpp(x, 0x141, 0xf, 0xf, false);  // lanes 0-7: all four groups of the row
+    return __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 16) + __builtin_amdgcn_readlane(x, 32) +
+           __builtin_amdgcn_readlane(x, 48);
+}
+
+// Per-wave LDS scratch of mode B: the tile's frame table (offset, length) for the full-piece
+// passes, the per-group full-piece counts, their inclusive prefix, and the piece slots.
+struct WaveScratch {
+    uint32_t ftab;   // [16] x {S_lo, S_hi, len, -}
+    uint32_t dpc;    // [16] pieces - 1
+    uint32_t epre;   // [16] inclusive prefix of dpc
+    uint32_t slots;  // [16 + 16 * kMaxFullPasses] x {Y, csum}
+};
+
+// Pass-0 rows over `ndp` stream dwords per group (whole frames in mode A, head pieces in mode B).
+__device__ __forceinline__ void pass0_unit(Unit& U, const Tile& T, int ndp, uint32_t gl,
+                                           const uint8_t* __restrict__ frames) {
+    const int rows0 = (ndp + kRowDwords - 1) / kRowDwords;
+    const int R0 = group_max(rows0);
+    U.P = (R0 + kPrefetch - 1) / kPrefetch * kPrefetch;
+    uint64_t ld_sdw = T.sdw();
+    int ld_nd = ndp;
+    {
+        const uint64_t ball = __ballot(rows0 == R0);  // never 0: some lane holds the maximum
+        const int src = (int)__builtin_ctzll(ball);
+        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ld_sdw, src);
+        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ld_sdw >> 32), src);
+        const int s_nd = __builtin_amdgcn_readlane(ndp, src);
+        if (ndp == 0) {
+            ld_sdw = ((uint64_t)s_hi << 32) | s_lo;
+            ld_nd = s_nd;
+        }
+    }
+    U.gfb = reinterpret_cast<const uint32_t*>(frames + (ld_sdw << 2));
+    U.rel0 = ld_nd - kRowDwords * U.P + 4 * (int)gl;
+    // Loads of rows that start before the frame are clamped to the frame's first chunk (its last
+    // chunk for frames under 4 dwords), so lanes idling through a tile's longest frame re-read
+    // one cached line instead of fetching the bytes that precede their frame; a chunk that
+    // straddles the frame start is loaded where it lies unless that is below frames[0].
+    U.lo = max(ld_sdw > (1u << 24) ? -(1 << 24) : -(int)ld_sdw, min(0, ld_nd - 4));
+    // Masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
+    // dword before the frame. The group's lane 0 has the lowest rel: row r is lean for the
+    // group once ndp - 16 P + 16 r >= 2.
+    const int need = 2 - (ndp - kRowDwords * U.P);
+    const int h = (ndp > 0 && need > 0) ? (need + kRowDwords - 1) / kRowDwords : 0;
+    U.H = min(group_max(h), U.P);
+    U.info = 0u;
+}
+
+__device__ __forceinline__ void tile_geometry(Tile& T, Unit& U, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
+                                              uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
+                                              char* lds, const WaveScratch& ws) {
+    T.len = (tile * kFramesPerTile + grp < n) ? len : 0u;
+    T.S = S;
+    const int nd = T.nd();
+    const int rows = (nd + kRowDwords - 1) / kRowDwords;
+    const int RA = (group_max(rows) + kPrefetch - 1) / kPrefetch * kPrefetch;
+    // mode B: pass 0 over the head pieces, then ceil(F / 16) full-piece passes of 12 rows, each
+    // about 2 rows' worth of combine; taken when that beats one pass over the longest frame
+    const int npc = nd > 0 ? pieces_of(nd) : 1;
+    const int nd0 = nd - kPieceDwords * (npc - 1);
+    const int P0B = (group_max((nd0 + kRowDwords - 1) / kRowDwords) + kPrefetch - 1) / kPrefetch * kPrefetch;
+    const int F = group_sum(npc - 1);
+    const int fullp = (F + kFramesPerTile - 1) / kFramesPerTile;
+    const bool modeB = F > 0 && fullp <= kMaxFullPasses && P0B + (kPieceRows + 2) * fullp < RA;
+    T.F = modeB ? F : 0;
+    T.npass = modeB ? 1 + fullp : 1;
+    if (modeB) {
+        // frame table, full-piece counts and their inclusive prefix (same wave: LDS in order)
+        if (gl == 0u) {
+            *reinterpret_cast<u32x4*>(lds + ws.ftab + 16u * grp) = u32x4{(uint32_t)S, (uint32_t)(S >> 32), T.len, 0u};
+            *reinterpret_cast<uint32_t*>(lds + ws.dpc + 4u * grp) = (uint32_t)(npc - 1);
+        }
+        int e = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kFramesPerTile; j += 4) {
+            const u32x4 d = *reinterpret_cast<const u32x4*>(lds + ws.dpc + 4u * j);
+            e += (j + 0 <= grp ? (int)d.x : 0) + (j + 1 <= grp ? (int)d.y : 0) + (j + 2 <= grp ? (int)d.z : 0) +
+                 (j + 3 <= grp ? (int)d.w : 0);
+        }
+        if (gl == 0u) *reinterpret_cast<uint32_t*>(lds + ws.epre + 4u * grp) = (uint32_t)e;
+    }
+    pass0_unit(U, T, modeB ? nd0 : nd, gl, frames);
+}
+
+// The full piece a group streams in pass p >= 1 (mode B): q = 16 (p - 1) + group; groups past
+// the tile's F pieces re-stream piece F - 1 (valid addresses) and discard it.
+__device__ __forceinline__ void full_piece_unit(Unit& U, const char* lds, const WaveScratch& ws,
+                                                const uint8_t* __restrict__ frames, int F, int p, uint32_t grp,
+                                                uint32_t gl) {
+    const int q0 = kFramesPerTile * (p - 1) + (int)grp;
+    const int q = min(q0, F - 1);
+    // frame i = #{j : E_j <= q}; its first full piece is number E_(i-1) = max{E_j : E_j <= q}
+    int i = 0, ebefore = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kFramesPerTile; j += 4) {
+        const u32x4 e = *reinterpret_cast<const u32x4*>(lds + ws.epre + 4u * j);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int ej = (int)e[c];
+            i += ej <= q ? 1 : 0;
+            ebefore = ej <= q ? max(ebefore, ej) : ebefore;
+        }
+    }
+    const u32x4 fr = *reinterpret_cast<const u32x4*>(lds + ws.ftab + 16u * (uint32_t)i);
+    const uint64_t S = ((uint64_t)fr.y << 32) | fr.x;
+    const uint32_t len = fr.z, sa = (uint32_t)S & 3u;
+    const int nd = (int)((sa + len + 3u) >> 2);
+    const int npc = pieces_of(nd);
+    const int k = q - ebefore + 1;                 // 1 .. npc - 1
+    U.gfb = reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2));
+    U.rel0 = nd - kPieceDwords * (npc - k) + 4 * (int)gl;  // the piece's first dword + the lane's chunk
+    U.lo = 0;
+    U.P = kPieceRows;
+    U.H = 0;
+    U.info = (q0 < F ? 0x80000000u : 0u) | (k == npc - 1 ? 0x40000000u : 0u) | (((sa + len) & 3u) << 28) |
+             (uint32_t)(kFramesPerTile + q);
+}
+
+// Would the tile run better in mode B? (the decision of tile_geometry, for the mode-A-only
+// kernel's report)
+__device__ __forceinline__ bool mode_b_worthy(int nd) {
+    const int rows = (nd + kRowDwords - 1) / kRowDwords;
+    const int RA = (group_max(rows) + kPrefetch - 1) / kPrefetch * kPrefetch;
+    const int npc = nd > 0 ? pieces_of(nd) : 1;
+    const int nd0 = nd - kPieceDwords * (npc - 1);
+    const int P0B = (group_max((nd0 + kRowDwords - 1) / kRowDwords) + kPrefetch - 1) / kPrefetch * kPrefetch;
+    const int F = group_sum(npc - 1);
+    const int fullp = (F + kFramesPerTile - 1) / kFramesPerTile;
+    return F > 0 && fullp <= kMaxFullPasses && P0B + (kPieceRows + 2) * fullp < RA;
+}
+
+// ---- the mode-A-only kernel's tile state: the group's own frame and its single pass
+struct TileA {
     uint64_t S;     // frame offset
     uint32_t len;   // frame length (0 for groups past the batch end)
     // row addressing: the group's own frame, or for an empty group a longest frame of the
@@ -432,36 +682,7 @@ struct Tile {
     }
 };
 
-__device__ __forceinline__ void tile_descriptors(uint32_t tile, uint32_t grp, uint32_t n,
-                                                 const uint64_t* __restrict__ offsets,
-                                                 const uint32_t* __restrict__ lengths, uint64_t& S, uint32_t& len) {
-    const uint32_t fi = tile * kFramesPerTile + grp;
-    // groups past the batch end read the last frame's descriptor (their length is zeroed)
-    const uint32_t fl = fi < n ? fi : n - 1u;
-    // Inline asm: hipcc otherwise sinks the loads into their first use, serializing two HBM
-    // round trips. The values are tied to an explicit wait (descriptors_ready) before use.
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(S) : "v"(offsets + fl));
-    asm volatile("global_load_dword %0, %1, off" : "=v"(len) : "v"(lengths + fl));
-}
-
-// vmcnt(0) tied to the descriptor registers, so no use of them is scheduled above it.
-__device__ __forceinline__ void descriptors_ready(uint64_t& S, uint32_t& len) {
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(S), "+v"(len));
-}
-
-// Wave max of a value that is uniform within each 4-lane group: two DPP row mirrors
-// combine the 4 groups of a 16-lane row, 4 readlanes the rows (no LDS permutes).
-__device__ __forceinline__ int group_max(int x) {
-    int y = __builtin_amdgcn_mov_dpp(x, 0x140, 0xf, 0xf, false);  // row_mirror
-    x = max(x, y);
-    y = __builtin_amdgcn_mov_dpp(x, 0x141, 0xf, 0xf, false);      // row_half_mirror
-    x = max(x, y);
-    const int a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
-    const int c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
-    return max(max(a, b), max(c, d));
-}
-
-__device__ __forceinline__ void tile_geometry(Tile& T, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
+__device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
                                               uint64_t S, uint32_t len, const uint8_t* __restrict__ frames) {
     T.len = (tile * kFramesPerTile + grp < n) ? len : 0u;
     T.S = S;
@@ -504,6 +725,16 @@ __device__ __forceinline__ int load_pos(int rel, int lo) { return rel <= -4 ? lo
 
 __device__ __forceinline__ u32x4 load_row(const uint32_t* fb, int pos) {
     return *reinterpret_cast<const u32x4_a4*>(fb + pos);
+}
+
+__device__ __forceinline__ void prefetch_unit(const Unit& U, u32x4 (&pf)[kPrefetch]) {
+    if (U.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
+#pragma unroll
+        for (int i = 0; i < kPrefetch; ++i) {
+            const int rel = U.rel0 + kRowDwords * i;
+            pf[i] = load_row(U.gfb, i < U.H ? load_pos(rel, U.lo) : rel);
+        }
+    }
 }
 
 // Region A in place: thread t builds Z64[b][e] (b = t >> 8, e = t & 255) as the XOR of
@@ -573,7 +804,8 @@ __device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, con
 // The tile's header slots: 8 dword DMAs; instruction i writes frame dword x = 4i + gl of
 // every group (lane-linear: LDS byte hw + 256 i + 4 lane). Sources are clamped to the
 // frame's last dword (never past it).
-__device__ __forceinline__ void header_dma(const Tile& T, const uint8_t* __restrict__ frames, const char* lds,
+template <class TileT>
+__device__ __forceinline__ void header_dma(const TileT& T, const uint8_t* __restrict__ frames, const char* lds,
                                            uint32_t hw, uint32_t gl) {
     const uint32_t hdr0 = __builtin_amdgcn_readfirstlane(lds_base(lds) + hw);
     const int last = T.ndall() - 1;
@@ -585,11 +817,41 @@ __device__ __forceinline__ void header_dma(const Tile& T, const uint8_t* __restr
     }
 }
 
+// 16-stream combine of a group's piece: U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3 per lane (minus the
+// junk the piece's last dword may carry, lane 3), Y = xor_l Z_16(3-l)(U_l) over the group by
+// DPP; the checksum partial folded mod 65535 (every partial < 2^18) and summed over the group.
+__device__ __forceinline__ void combine_piece(const char* lds, uint32_t gl, const uint32_t (&A)[4], uint32_t cs,
+                                              uint32_t junk, uint32_t& Y, uint32_t& csum) {
+    const uint32_t U =
+        zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3] ^ junk;
+    cs -= sad16(junk, 0u);
+    const uint32_t ybase = (gl == 0u) ? kLdsZ48 : (gl == 1u) ? kLdsZ32 : kLdsZ16;
+    uint32_t y = zplain(lds, U, ybase);
+    if (gl == 3u) y = U;
+    y ^= dpp_quad<kQuadXor1>(y);
+    y ^= dpp_quad<kQuadXor2>(y);
+    cs = (cs & 0xffffu) + (cs >> 16);
+    cs += dpp_quad<kQuadXor1>(cs);
+    cs += dpp_quad<kQuadXor2>(cs);
+    Y = y;
+    csum = cs;
+}
+
+// `report` = the host-mapped report word's address in bits 0..47, the launch id in bits 48..63
+// (one kernel argument, loaded where it is used: nothing of it stays live through the tile loop).
+__device__ __forceinline__ void post_report(uint64_t report) {
+    asm volatile("" : "+s"(report));  // split here, not hoisted into a register held by the whole kernel
+    *reinterpret_cast<uint32_t*>(report & 0xFFFFFFFFFFFFull) = (uint32_t)(report >> 48);
+}
+
+// The kernel for batches of similar lengths: every tile in mode A (one pass). It reports in
+// `report` whether any tile would have run better in mode B, so that the host launches
+// digest_kernel_ab next time (launch_digest).
 __global__ void __launch_bounds__(kThreads, 1)
-digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
-              const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
-              uint2* __restrict__ out, uint8_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+                const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
+                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report) {
+    char* lds = g_lds;
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
@@ -620,7 +882,7 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
     uint32_t tile = gwave;
     FS_RTSTAMP(5);
     FS_STAMP(0);
-    Tile T;
+    TileA T;
     u32x4 pf[kPrefetch];
     const bool first = __builtin_amdgcn_readfirstlane(tile) < ntiles;
     {
@@ -630,7 +892,10 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         build_region_a(tabs, lds);
         descriptors_ready(S, len);
         T.P = 0;
-        if (first) tile_geometry(T, tile, grp, gl, n, S, len, frames);
+        if (first) {
+            tile_geometry_a(T, tile, grp, gl, n, S, len, frames);
+            if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+        }
     }
     plain_dma(tabs, lds, wave, lane);
     if (first) {
@@ -667,26 +932,8 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
         auto parse = [&](bool refilled) {
             if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
             else __builtin_amdgcn_s_waitcnt(0x0070);
-            // group-vectorised sums over the slot (all lanes of valid groups take part)
-            const uint32_t sa = T.sa(), len = T.len;
-            const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2));
-            const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3));
-            const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
-            const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 4)) >> 16;
-            const uint32_t end = (14u + tl) & 0xffffu;
-            // [0, off) spans at most 3 + 74 bytes: absolute dwords < 20
-            const uint32_t hsum = slot_sum(lds, hw, grp, gl, sa, 0, (int)min(off, len), 5);
-            const bool pad_in_slot = sa + len <= 4u * kHdrDwords;
-            int64_t pad = -1;
-            if (__ballot(len >= 34u && end < len && pad_in_slot) != 0) {
-                const uint32_t ps = slot_sum(lds, hw, grp, gl, sa, (int)min(end, len), (int)len, kHdrDwords / 4);
-                if (pad_in_slot) pad = (int64_t)ps;
-            }
-#ifndef FS_NOPARSE
-            if (parser) park_parsed(lds, hw, grp, parse_frame(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
-#else
-            if (parser) *reinterpret_cast<uint32_t*>(lds + hdr_at(hw, grp, 0)) = hsum + (uint32_t)pad;
-#endif
+            parse_tile(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
+                       parser);
         };
         auto prio = [&](int r0) {
             // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
@@ -808,7 +1055,8 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
             uint32_t len;
             tile_descriptors(tile, grp, n, offsets, lengths, S, len);
             descriptors_ready(S, len);
-            tile_geometry(T, tile, grp, gl, n, S, len, frames);
+            tile_geometry_a(T, tile, grp, gl, n, S, len, frames);
+            if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             header_dma(T, frames, lds, hw, gl);
             if (T.P > 0) {
 #pragma unroll
@@ -817,6 +1065,254 @@ digest_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ o
                     pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
                 }
             }
+        }
+    }
+}
+
+// The kernel for batches with mixed lengths: tiles in mode A or mode B, per tile.
+__global__ void __launch_bounds__(kThreads, 1)
+digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+                 const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
+                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report) {
+    char* lds = g_lds;
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR addresses
+    const uint32_t grp0 = lane >> 2;   // frame slot of this lane's group
+    const uint32_t gl0 = lane & 3u;    // lane within the group
+    const uint32_t gwave = blockIdx.x * kWavesPerBlock + wave;
+    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+    const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
+    const uint32_t hw = kLdsHdr + wave * kHdrWaveBytes;  // this wave's header slots
+    WaveScratch ws;
+    ws.ftab = kLdsWave + wave * kWaveScratchBytes;
+    ws.dpc = ws.ftab + 16u * kFramesPerTile;
+    ws.epre = ws.dpc + 4u * kFramesPerTile;
+    ws.slots = ws.epre + 4u * kFramesPerTile;
+
+    LaneKeys keys;
+    {
+        const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
+        keys.cvec = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) keys.cvec |= (32u * j + 4u * c) << (8u * j);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t b = (k + h) & 3u;
+            keys.sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
+        }
+    }
+
+    // Preamble: the first tile's descriptors (the first memory ops, one round trip) while
+    // region A is built in place by VALU; geometry; the plain tables' LDS-DMA (40 KB, L2
+    // hits); the header DMA; the row prefetch; one barrier once this wave's table pieces
+    // have landed.
+    uint32_t tile = gwave;
+    FS_RTSTAMP(5);
+    FS_STAMP(0);
+    Tile T;
+    Unit U;
+    u32x4 pf[kPrefetch];
+    const bool first = __builtin_amdgcn_readfirstlane(tile) < ntiles;
+    {
+        uint64_t S;
+        uint32_t len;
+        tile_descriptors(tile, grp0, n, offsets, lengths, S, len);
+        build_region_a(tabs, lds);
+        descriptors_ready(S, len);
+        U.P = 0;
+        if (first) tile_geometry(T, U, tile, grp0, gl0, n, S, len, frames, lds, ws);
+    }
+    plain_dma(tabs, lds, wave, lane);
+    if (first) {
+        header_dma(T, frames, lds, hw, gl0);
+        prefetch_unit(U, pf);
+    }
+    FS_STAMP(9);
+    // the table pieces are older than the header DMA and the rows: vmcnt(header + rows);
+    // lgkmcnt(0): this wave's region-A stores
+    // s_waitcnt field layout (gfx9): vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4], lgkmcnt[11:8]
+    if (first && U.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | (kPrefetch + kHdrDmas));
+    else if (first) __builtin_amdgcn_s_waitcnt(0x0070 | kHdrDmas);
+    else __builtin_amdgcn_s_waitcnt(0x0070);
+    FS_STAMP(10);
+    __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    FS_STAMP(1);
+
+    while (tile < ntiles) {
+        // Opaque copies of the lane indices: everything derived from them is recomputed per
+        // tile instead of being hoisted out of the tile loop into (spilled) registers.
+        uint32_t grp = grp0, gl = gl0;
+        asm volatile("" : "+v"(grp), "+v"(gl));
+        const bool fvalid = tile * kFramesPerTile + grp < n;
+        const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
+        const int npass = T.npass;
+        const int total_rows = U.P + kPieceRows * (npass - 1);
+        if (npass > 1 && lane == 0u && report) post_report(report);  // this launch met a mixed tile
+
+        // ---- header parse: after the first block of rows, while the ring's loads are in flight.
+        // The header DMA was issued before the tile's rows; vmcnt(kPrefetch) retires it once the
+        // first block's refills are the only younger loads.
+        auto parse = [&](bool refilled) {
+            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
+            else __builtin_amdgcn_s_waitcnt(0x0070);
+            parse_tile(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
+                       parser);
+        };
+        uint32_t Y = 0u, csum = 0u;  // the frame's combined register value and sum (mode A)
+        for (int pass = 0; pass < npass; ++pass) {
+            // (opaque per pass too: lane-derived row constants are rematerialized per pass)
+            asm volatile("" : "+v"(grp), "+v"(gl));
+            uint32_t A[4] = {0u, 0u, 0u, 0u};
+            uint32_t cs = 0u;
+            const int done0 = pass == 0 ? 0 : U.P == 0 ? 0 : (total_rows - kPieceRows * (npass - pass));
+            auto prio = [&](int r0) {
+                // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
+                // a wave with more rows left gets a higher priority.
+                if (FS_PRIO && total_rows > 36) {  // long tiles only (C2-size tiles run faster without)
+                    const int left4 = 4 * (total_rows - done0 - r0);  // vs quarters of total_rows
+                    if (left4 > 3 * total_rows) __builtin_amdgcn_s_setprio(3);
+                    else if (left4 > 2 * total_rows) __builtin_amdgcn_s_setprio(2);
+                    else if (left4 > total_rows) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
+            };
+            // general block: rows below H take the masked path (scalar branch per row); refills
+            // of rows below H are clamped
+            auto block = [&](int r0, auto refill_tag) {
+                constexpr bool kRefill = decltype(refill_tag)::value;
+                prio(r0);
+#pragma unroll
+                for (int i = 0; i < kPrefetch; ++i) {
+                    const int r = r0 + i;
+                    const int rel = U.rel0 + kRowDwords * r;
+                    // consume the ring slot, then refill the SAME registers: no copy of an
+                    // in-flight load, so the compiler keeps kPrefetch-1 loads outstanding
+                    if (r < U.H) masked_row(lds, keys, pf[i], rel, load_pos(rel, U.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
+                    else lean_row(lds, keys, pf[i], A, cs);
+                    if (kRefill) {
+                        const int rn = rel + kRowDwords * kPrefetch;
+                        pf[i] = load_row(U.gfb, r + kPrefetch < U.H ? load_pos(rn, U.lo) : rn);
+                    }
+                }
+            };
+            // lean block: every row lean for every lane; the refills lie inside the frame, so they
+            // need no clamp: one pointer per block, immediate row offsets
+            auto lean_block = [&](int r0, auto refill_tag) {
+                constexpr bool kRefill = decltype(refill_tag)::value;
+                prio(r0);
+                const uint32_t* pb = U.gfb + (U.rel0 + kRowDwords * (r0 + kPrefetch));
+#pragma unroll
+                for (int i = 0; i < kPrefetch; ++i) {
+                    lean_row(lds, keys, pf[i], A, cs);
+                    if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
+                    // keep consume/refill interleaved per row: unfenced, the scheduler sinks all
+                    // refills to the block end behind a vmcnt(0), draining the ring every block
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            };
+            using Yes = std::true_type;
+            using No = std::false_type;
+            const int Rc = U.P - kPrefetch;  // first row of the last block
+            if (U.P > 0) {
+                // [first block] (pass 0: parse) [head blocks: general] [body: lean] [last block]
+                if (Rc > 0) {
+                    if (U.H > 0) block(0, Yes());
+                    else lean_block(0, Yes());
+                    if (pass == 0) parse(true);
+                    int r0 = kPrefetch;
+                    for (; r0 < Rc && r0 < U.H; r0 += kPrefetch) block(r0, Yes());
+                    for (; r0 < Rc; r0 += kPrefetch) lean_block(r0, Yes());
+                    if (Rc < U.H) block(Rc, No());
+                    else lean_block(Rc, No());
+                } else {
+                    if (U.H > 0) block(0, No());
+                    else lean_block(0, No());
+                    if (pass == 0) parse(false);
+                }
+            } else {
+                parse(false);  // no rows (every frame of the tile under 4 bytes): rejected by length
+            }
+            FS_STAMP(2);
+            // Opaque frame descriptor: what the combine and the finish derive from it is
+            // recomputed here rather than kept (and spilled) across the row loop.
+            asm volatile("" : "+v"(T.S), "+v"(T.len));
+            // The pass's last row was lean (unless every row was masked): if it ends the frame,
+            // its last dword -- lane 3's 4th -- still holds the up to 3 bytes past the frame end.
+            // Their CRC contribution is that junk itself (the last dword enters the combine
+            // unshifted) and their sum is sad16 of it: combine_piece removes both.
+            uint32_t junk = 0u;
+            if (pass == 0) {
+                // mode B: a head piece ends the frame only when it is the whole frame
+                const bool ends = npass == 1 || pieces_of(T.nd()) == 1;
+                if (U.P > 0 && U.H < U.P && gl == 3u && T.nd() > 0 && ends) junk = pf[kPrefetch - 1].w & ~T.tail_mask();
+            } else if ((U.info & 0x40000000u) && gl == 3u) {
+                const uint32_t t = (U.info >> 28) & 3u;
+                junk = pf[kPrefetch - 1].w & ~(t == 0u ? 0xffffffffu : ((1u << (8u * t)) - 1u));
+            }
+            const uint32_t info = U.info;
+            // the next pass's piece and its first rows, in flight during this pass's combine
+            if (pass + 1 < npass) {
+                full_piece_unit(U, lds, ws, frames, T.F, pass + 1, grp, gl);
+                prefetch_unit(U, pf);
+            }
+            uint32_t y, c;
+            combine_piece(lds, gl, A, cs, junk, y, c);
+            if (npass == 1) {
+                Y = y;
+                csum = c;
+            } else if (gl == 0u && (pass == 0 || (info >> 31))) {
+                const uint32_t slot = pass == 0 ? grp : (info & 0xffffu);
+                *reinterpret_cast<uint2*>(lds + ws.slots + 8u * slot) = make_uint2(y, c);
+            }
+        }
+        FS_STAMP(3);
+        // ---- the group's lane 0: (mode B) Horner over the frame's pieces, finish and store
+        // (its frame's parse comes back from LDS).
+        if (parser) {
+            if (npass > 1) {
+                const uint2 h = *reinterpret_cast<const uint2*>(lds + ws.slots + 8u * grp);
+                Y = h.x;
+                csum = h.y;
+                const int npc = pieces_of(T.nd());
+                // the frame's first full piece: the exclusive prefix of the groups' full pieces
+                const int e0 = (int)lds32(lds, ws.epre + 4u * grp) - (npc - 1);
+                for (int k = 1; k < npc; ++k) {
+                    const uint2 sl = *reinterpret_cast<const uint2*>(lds + ws.slots + 8u * (kFramesPerTile + e0 + k - 1));
+                    Y = zplain(lds, Y, kLdsZ768) ^ sl.x;
+                    csum += sl.y;
+                }
+            }
+            const Parsed P = unpark_parsed(lds, hw, grp);
+            const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2));
+            uint32_t crcv;
+            if (T.len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
+                uint32_t c = 0xffffffffu;
+                const uint8_t* fbytes = frames + T.S;
+                for (uint32_t p = 0; p < T.len; ++p)
+                    c = lds32(lds, kLdsZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
+                crcv = ~c;
+            } else {
+                const uint32_t tpad = (4u - T.te()) & 3u;  // zero bytes appended by the dword rounding
+                crcv = ~zplain(lds, Y, kLdsZfin + 4096u * tpad);
+            }
+            uint32_t verdict = P.verdict, l4 = 0u;
+            if (P.compute) l4 = finish_l4(fbs, T.sa(), T.len, P, csum, verdict);
+            const uint32_t fi = tile * kFramesPerTile + grp;
+            out[fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
+            if (status) status[fi] = (uint8_t)verdict;
+        }
+        FS_STAMP(4);
+        FS_RTSTAMP(6);
+        tile += nwaves;
+        if (tile < ntiles) {  // next tile: descriptors, geometry, header DMA, row prefetch
+            uint64_t S;
+            uint32_t len;
+            tile_descriptors(tile, grp, n, offsets, lengths, S, len);
+            descriptors_ready(S, len);
+            tile_geometry(T, U, tile, grp, gl, n, S, len, frames, lds, ws);
+            header_dma(T, frames, lds, hw, gl);
+            prefetch_unit(U, pf);
         }
     }
 }
@@ -831,14 +1327,36 @@ extern "C" int fs_debug_read_stamps(void* host, size_t bytes) {
 
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
-                         int num_cus) {
+                         int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force) {
     if (n == 0) return hipSuccess;
     const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
     uint32_t blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t max_blocks = (uint32_t)(num_cus > 0 ? num_cus : 256);
     if (blocks > max_blocks) blocks = max_blocks;
-    hipLaunchKernelGGL(digest_kernel, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu,
-                       tables, reinterpret_cast<uint2*>(out), status);
+    // The report of the launches before (the latest launch id that met a mixed-length tile):
+    // launches are enqueued ahead of the GPU, so a report arrives several launches late; the
+    // mixed kernel stays chosen for kStickyLaunches launches after the latest report (it keeps
+    // reporting while the traffic is mixed). A heuristic only: never a result.
+    // Launch ids are 16-bit (they travel in the report pointer's top bits; 0 = never reported).
+    constexpr uint32_t kStickyLaunches = 4096;
+    static std::atomic<uint32_t> next_id{1};
+    uint32_t id = next_id.fetch_add(1) & 0xFFFFu;
+    if (id == 0u) id = next_id.fetch_add(1) & 0xFFFFu;
+    const uint64_t rdev = reinterpret_cast<uint64_t>(report_dev);
+    const bool can_report = report_host && rdev != 0u && (rdev >> 48) == 0u;
+    const uint64_t report = can_report ? rdev | ((uint64_t)id << 48) : 0u;
+    bool mixed = false;
+    if (can_report) {
+        const uint32_t latest = *report_host;
+        mixed = latest != 0u && ((id - latest) & 0xFFFFu) <= kStickyLaunches;
+    }
+    if (force) mixed = force == 2;
+    if (mixed)
+        hipLaunchKernelGGL(digest_kernel_ab, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu,
+                           tables, reinterpret_cast<uint2*>(out), status, report);
+    else
+        hipLaunchKernelGGL(digest_kernel_a, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu,
+                           tables, reinterpret_cast<uint2*>(out), status, report);
     return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ void build_tables(FsTables* t) {
     op_table(t1, 48, t->z48);
     op_table(t1, 12, t->z12);
     op_table(t1, 8, t->z8);
+    op_table(t1, 768, t->z768);
     // The final step Z_(4-t) replaces "Z_4 then undo t appended zero bytes"; Z_1[0] is the
     // standard byte table used for frames shorter than 4 bytes.
     if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");

@@ -56,6 +56,7 @@ EXPORTED_SYMBOLS = (
     "fs_last_error",
     "fs_digest_batch",
     "fs_digest_batch_host",
+    "fs_ctx_set_kernel",
     "fs_host_alloc",
     "fs_host_free",
 )
@@ -97,6 +98,8 @@ def load_library() -> ctypes.CDLL:
     lib.fs_digest_batch.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp]
     lib.fs_digest_batch_host.restype = i32
     lib.fs_digest_batch_host.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp, vp]
+    lib.fs_ctx_set_kernel.restype = i32
+    lib.fs_ctx_set_kernel.argtypes = [vp, ctypes.c_int]
     lib.fs_host_alloc.restype = i32
     lib.fs_host_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
     lib.fs_host_free.restype = i32
@@ -149,6 +152,14 @@ class Engine:
     def _check(self, st: int, what: str) -> None:
         if st != FS_SUCCESS:
             raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
+
+    # kernel variants (fs_ctx_set_kernel): results are identical, only the speed differs
+    KERNEL_AUTO, KERNEL_ONE_PASS, KERNEL_MIXED = 0, 1, 2
+
+    def set_kernel(self, variant: int) -> None:
+        """0: pick per launch from the previous launches' report (default); 1: the one-pass
+        kernel; 2: the kernel that splits long frames of mixed-length tiles into pieces."""
+        self._check(self.lib.fs_ctx_set_kernel(self._ctx, int(variant)), "fs_ctx_set_kernel")
 
     # ---- device-resident path (torch tensors as device memory) -------------
     def digest_device(self, frames, offsets, lengths, mtu: int = 0, out=None, status=None, stream=None):

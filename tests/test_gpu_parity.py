@@ -21,11 +21,14 @@ from seqs_amd import Engine, pack_frames, split_digests, synth  # noqa: E402
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(scope="module")
-def engine():
+@pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_AUTO],
+                ids=["one_pass", "mixed", "auto"])
+def engine(request):
+    # every case through both kernel variants (and the automatic choice between them)
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     e = Engine(0)
+    e.set_kernel(request.param)
     yield e
     e.close()
 
@@ -193,6 +196,33 @@ def test_host_staged_multichunk_unordered(engine):
     pin[:] = buf
     dig2, st2 = engine.digest_host(pin, off, ln)
     assert np.array_equal(dig2, edig) and np.array_equal(st2, est)
+
+
+def test_piece_boundaries_and_mixed_tiles(engine):
+    # Mixed tiles (mode B): a jumbo frame beside short ones at every start alignment, lengths
+    # around the 768-byte piece boundaries (stream dwords = 192 k + {0, 1, 2, 3}), frames whose
+    # Ethernet padding lies in their last piece or past the header slot, tiles whose full pieces
+    # do not fill the last pass, and a tile with more full pieces than the passes allow.
+    import random
+
+    import framegen
+
+    rnd = random.Random(11)
+    frames = []
+    for k in range(1, 13):
+        for d in (-5, -4, -3, -2, -1, 0, 1, 2, 3, 4, 5):
+            L = 768 * k + d
+            frames.append(framegen.valid_frame(rnd, 6 if (k + d) % 2 else 17, payload=max(0, L - 54)))
+            frames.append(bytes(rnd.randbytes(max(1, 60 + d))))
+    for pad in (1, 46, 300, 2000):
+        frames.append(framegen.valid_frame(rnd, 6, payload=3000, pad=pad))
+        frames.append(framegen.valid_frame(rnd, 17, payload=20, pad=pad))
+    frames += [framegen.valid_frame(rnd, 6, payload=9000 - 54) for _ in range(3)] + [b"\x01" * 64] * 13
+    frames += [bytes(rnd.randbytes(100000))] + [b"\x02" * 60] * 15  # too many full pieces: one pass
+    for align in (1, 4):
+        buf, off, ln = pack_frames(frames, align=align)
+        check(engine, buf, off, ln, label=f"pieces/align{align}")
+        check(engine, buf, off, ln, mtu=1514, label=f"pieces/align{align}/mtu")
 
 
 def test_host_staged_rejects_out_of_range(engine):

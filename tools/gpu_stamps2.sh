@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 for v in "$@"; do
-  for cfg in c2 c3; do
+  for cfg in c2; do
     echo "== $v $cfg"
     FRAMESUM_LIB="$GRAFT_REPO_ROOT/seqs_amd/lib/diag/libframesum_$v.so" timeout -k 10 120 python tools/stamps.py --config $cfg > gpurun_out/stamps_${v}_$cfg.log 2>&1 || { echo "STAMPS FAILED"; tail -5 gpurun_out/stamps_${v}_$cfg.log; exit 1; }
     grep -v amdgpu.ids gpurun_out/stamps_${v}_$cfg.log
