@@ -6,6 +6,10 @@ usage: prof_summary.py <collection dir (gpurun_out/prof)> <output dir>
 Writes, per config (c2, c3):
   kernel_stats_<cfg>.csv   rocprofv3 --kernel-trace --stats summary of the bench.py command
   bench_<cfg>.json         the bench line printed by that same command
+  trace_<cfg>.json         kernel durations from that command's kernel trace: all dispatches, and the
+                           last `steps` ones = bench.py's single-stream event-timed pass (the one its
+                           roofline.kernel_avg_us comes from; the timed loop's 2-stream overlap makes
+                           individual durations longer there), next to the bench's own figure
   pmc_<cfg>.json           per-dispatch medians of every PMC counter for digest_kernel, plus
                            hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
                            (FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE reads 1/2 of a wide
@@ -37,6 +41,29 @@ def counters(pass_dir):
     return {k: statistics.median(v) for k, v in by_name.items()}, {k: len(v) for k, v in by_name.items()}
 
 
+def trace_timing(trace_csv, bench):
+    durs = []
+    with open(trace_csv) as f:
+        for row in csv.DictReader(f):
+            if KERNEL in row["Kernel_Name"]:
+                durs.append((int(row["Dispatch_Id"]), int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+    durs.sort()
+    spans = [(a, b) for _, a, b in durs]
+    durs = [b - a for _, a, b in durs]
+    steps = int(bench.get("steps", 0)) if bench else 0
+    last = durs[-steps:] if steps else []
+    us = lambda v: round(v / 1e3, 3)
+    out = {"kernel": KERNEL, "dispatches": len(durs), "all_avg_us": us(statistics.mean(durs)) if durs else None}
+    if last:
+        out.update({"single_stream_pass_dispatches": len(last), "single_stream_pass_avg_us": us(statistics.mean(last)),
+                    "single_stream_pass_median_us": us(statistics.median(last))})
+        # first start to last end of the pass, per launch: what the bench's one event pair measures
+        out["single_stream_pass_span_per_launch_us"] = us((spans[-1][1] - spans[-len(last)][0]) / len(last))
+    if bench:
+        out["bench_kernel_avg_us"] = bench["roofline"]["kernel_avg_us"]
+    return out
+
+
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     os.makedirs(dst, exist_ok=True)
@@ -50,6 +77,13 @@ def main():
             if lines:
                 with open(os.path.join(dst, f"bench_{cfg}.json"), "w") as f:
                     f.write(lines[-1] + "\n")
+                traces = glob.glob(os.path.join(src, cfg, "**", "*kernel_trace.csv"), recursive=True)
+                if traces:
+                    tt = trace_timing(traces[0], json.loads(lines[-1]))
+                    with open(os.path.join(dst, f"trace_{cfg}.json"), "w") as f:
+                        json.dump(tt, f, indent=1)
+                        f.write("\n")
+                    print(cfg, json.dumps(tt))
         med, n = {}, {}
         for d in sorted(glob.glob(os.path.join(src, f"pmc_{cfg}_*"))):
             if os.path.isdir(d):
