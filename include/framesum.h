@@ -69,7 +69,9 @@ enum fs_verdict {
     FS_ERR_ZERO_PORT = 10,              /* errZeroPort */
     FS_ERR_BAD_UDP_LENGTH = 11,         /* errBadUDPLength */
     FS_ERR_BAD_TCP_OFFSET = 12,         /* errBadTCPOffset */
-    FS_ERR_CHECKSUM = 13                /* ErrChecksumTCPorUDP */
+    FS_ERR_CHECKSUM = 13,               /* ErrChecksumTCPorUDP */
+    FS_ERR_FCS = 14                     /* fs_digest_batch_fcs only: FCS missing or wrong (the
+                                           frame is dropped before RecvEth; not in the reference) */
 };
 
 /* 8-byte per-frame digest. crc32: IEEE CRC-32 of frame[0:len).
@@ -104,6 +106,35 @@ const char* fs_last_error(const fs_ctx* ctx);
  * Asynchronous on `stream` (a hipStream_t; NULL = the null stream). */
 fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths,
                           uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status, void* stream);
+
+/* TX checksum fill, device-resident and in place. The
+ * reference fills a frame's checksums while it builds the frame from header structs:
+ *   stacks/port_tcp.go:178 `pkt.IP.Checksum = pkt.IP.CalculateChecksum()` and :193
+ *   `pkt.TCP.Checksum = pkt.TCP.CalculateChecksumIPv4(&pkt.IP, nil, payload)`;
+ *   stacks/dhcp_client.go:479/:486 and dhcp_server.go:203/:216 (IP, then UDP).
+ * For frames whose headers are already in place, flags:
+ *   FS_FILL_CSUM  writes the IPv4 header checksum (eth/headers.go:333-340) to frame[24:26]
+ *                 and the TCP/UDP checksum RecvEth verifies (the same arithmetic, with the
+ *                 frame's own TCP options; none when the data offset is 5, as :193 passes
+ *                 nil) to the L4 checksum field, both big-endian, for every frame whose
+ *                 RecvEth evaluation reaches the checksum compare (verdict FS_OK or
+ *                 FS_ERR_CHECKSUM before the fill); other frames are not written.
+ *   FS_FCS_APPEND writes the IEEE CRC-32 of the frame (as filled) little-endian at
+ *                 frame[len:len+4), the FCS in wire order: those 4 bytes must be spare
+ *                 (part of no frame of the batch).
+ * out/status receive what fs_digest_batch would report for the frames as written (filled
+ * frames: FS_OK). Frames must not overlap. Asynchronous on `stream`. */
+#define FS_FILL_CSUM 1u
+#define FS_FCS_APPEND 2u
+fs_status fs_fill_batch(fs_ctx* ctx, uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                        uint32_t mtu, uint32_t flags, fs_digest* out, uint8_t* status, void* stream);
+
+/* RX of raw wire frames that still carry their 4-byte FCS (NICs that do not strip it;
+ * SURVEY.md §8f rank 4, not in the reference): lengths[i] includes the FCS. out/status are
+ * fs_digest_batch's for frame[0:len-4), the bytes RecvEth would receive, except that status
+ * is FS_ERR_FCS when len < 4 or the little-endian FCS differs from that CRC-32. */
+fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths,
+                              uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status, void* stream);
 
 /* Same computation from/to HOST memory (the NIC / loopback buffer handed to
  * RecvEth): stages H2D, runs the kernel and copies D2H on the context's

@@ -45,6 +45,10 @@ def load() -> ctypes.CDLL:
     lib.oracle_recv_eth.argtypes = [vp, sz, u32, ctypes.POINTER(u16), ctypes.POINTER(u16)]
     lib.oracle_digest_batch.restype = None
     lib.oracle_digest_batch.argtypes = [vp, vp, vp, u32, u32, ctypes.c_int, ctypes.c_int, vp, vp]
+    lib.oracle_fill_batch.argtypes = [vp, vp, vp, u32, u32, u32, vp, vp]
+    lib.oracle_fill_batch.restype = None
+    lib.oracle_digest_fcs_batch.argtypes = [vp, vp, vp, u32, u32, ctypes.c_int, vp, vp]
+    lib.oracle_digest_fcs_batch.restype = None
     lib.oracle_crc791_reset.argtypes = [vp]
     lib.oracle_crc791_write.restype = sz
     lib.oracle_crc791_write.argtypes = [vp, vp, sz]
@@ -109,6 +113,11 @@ class CRC791:
         return int(load().oracle_crc791_sum16(self._st))
 
 
+FILL_CSUM = 1
+FCS_APPEND = 2
+FS_ERR_FCS = 14
+
+
 def digest_batch(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, mtu: int = 0,
                  use_zlib: bool = True, nthreads: int = 1):
     """Oracle digests for a packed batch: returns (digests[DIGEST_DTYPE], status u8)."""
@@ -121,5 +130,37 @@ def digest_batch(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, mtu:
     load().oracle_digest_batch(
         buf.ctypes.data_as(ctypes.c_void_p), offsets.ctypes.data_as(ctypes.c_void_p),
         lengths.ctypes.data_as(ctypes.c_void_p), n, mtu, 1 if use_zlib else 0, nthreads,
+        out.ctypes.data_as(ctypes.c_void_p), st.ctypes.data_as(ctypes.c_void_p))
+    return out, st
+
+
+def fill_batch(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, mtu: int = 0, flags: int = FILL_CSUM):
+    """Oracle TX fill IN PLACE on `buf` (a writable uint8 array): checksums into the frames
+    (FILL_CSUM) and/or the FCS after each frame (FCS_APPEND). Returns (digests, status) of
+    the frames as they are afterwards."""
+    assert buf.dtype == np.uint8 and buf.flags["C_CONTIGUOUS"] and buf.flags["WRITEABLE"]
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = int(lengths.size)
+    out = np.zeros(n, dtype=DIGEST_DTYPE)
+    st = np.zeros(n, dtype=np.uint8)
+    load().oracle_fill_batch(
+        buf.ctypes.data_as(ctypes.c_void_p), offsets.ctypes.data_as(ctypes.c_void_p),
+        lengths.ctypes.data_as(ctypes.c_void_p), n, mtu, flags,
+        out.ctypes.data_as(ctypes.c_void_p), st.ctypes.data_as(ctypes.c_void_p))
+    return out, st
+
+
+def digest_fcs_batch(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, mtu: int = 0, nthreads: int = 1):
+    """Oracle RX digests of wire frames that carry a trailing 4-byte FCS (lengths include it)."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = int(lengths.size)
+    out = np.zeros(n, dtype=DIGEST_DTYPE)
+    st = np.zeros(n, dtype=np.uint8)
+    load().oracle_digest_fcs_batch(
+        buf.ctypes.data_as(ctypes.c_void_p), offsets.ctypes.data_as(ctypes.c_void_p),
+        lengths.ctypes.data_as(ctypes.c_void_p), n, mtu, nthreads,
         out.ctypes.data_as(ctypes.c_void_p), st.ctypes.data_as(ctypes.c_void_p))
     return out, st

@@ -239,18 +239,86 @@ void oracle_frame_digest(const uint8_t* f, size_t len, uint32_t mtu, int use_zli
     if (status) *status = st;
 }
 
+/* ---------------------------------------------------------------------- */
+/* TX checksum fill. The reference fills a frame's checksums while
+ * building it from header structs:
+ *   TCP: stacks/port_tcp.go:178  pkt.IP.Checksum = pkt.IP.CalculateChecksum()
+ *        stacks/port_tcp.go:193  pkt.TCP.Checksum = pkt.TCP.CalculateChecksumIPv4(&pkt.IP, nil, payload)
+ *   UDP: stacks/dhcp_client.go:479 / :486 and dhcp_server.go:203 / :216 (IP, then UDP)
+ * Batched over frames whose headers are already in place, the same arithmetic is the one
+ * RecvEth verifies (portstack.go:239 / :303, with the frame's own TCP options, nil when
+ * the data offset is 5): the IPv4 header checksum goes to frame[24:26] and the computed
+ * L4 checksum to the L4 header's checksum field (TCP +16, UDP +6), both big-endian, for
+ * every frame whose RecvEth evaluation reaches the checksum compare (FS_OK or
+ * FS_ERR_CHECKSUM); other frames are left as they are. Neither written field enters its
+ * own checksum, so after the fill RecvEth accepts the frame. The digest and verdict
+ * reported are those of the frame as it is afterwards; with ORACLE_FCS_APPEND the
+ * frame's IEEE CRC-32 is also written little-endian at frame[len:len+4) (FCS order on the
+ * wire). */
+void oracle_fill_frame(uint8_t* f, size_t len, uint32_t mtu, uint32_t flags, oracle_digest* d, uint8_t* status) {
+    uint16_t ipc, l4c;
+    uint8_t st = oracle_recv_eth(f, len, mtu, &ipc, &l4c);
+    if ((flags & ORACLE_FILL_CSUM) && (st == FS_OK || st == FS_ERR_CHECKSUM)) {
+        size_t off = 14 + (size_t)(f[14] & 0xf) * 4;
+        size_t field = off + (f[14 + 9] == 6 ? 16 : 6);
+        f[24] = (uint8_t)(ipc >> 8);
+        f[25] = (uint8_t)ipc;
+        f[field] = (uint8_t)(l4c >> 8);
+        f[field + 1] = (uint8_t)l4c;
+        st = oracle_recv_eth(f, len, mtu, &ipc, &l4c);
+    }
+    d->crc32 = oracle_crc32_zlib(f, len);
+    d->ip_csum = ipc;
+    d->l4_csum = l4c;
+    if (flags & ORACLE_FCS_APPEND) {
+        for (int b = 0; b < 4; b++) f[len + b] = (uint8_t)(d->crc32 >> (8 * b));
+    }
+    if (status) *status = st;
+}
+
+void oracle_fill_batch(uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint32_t mtu,
+                       uint32_t flags, oracle_digest* out, uint8_t* status) {
+    for (uint32_t i = 0; i < n; i++)
+        oracle_fill_frame(frames + offsets[i], lengths[i], mtu, flags, &out[i], status ? &status[i] : NULL);
+}
+
+/* RX of a raw wire frame that still carries its 4-byte FCS (little-endian IEEE CRC-32 of the
+ * bytes before it; SURVEY.md §8f rank 4, not in the reference): the digest and RecvEth
+ * verdict of frame[0:len-4), the bytes a NIC that strips the FCS would hand to RecvEth,
+ * with the verdict replaced by FS_ERR_FCS when the FCS is missing (len < 4) or differs. */
+void oracle_frame_digest_fcs(const uint8_t* f, size_t len, uint32_t mtu, oracle_digest* d, uint8_t* status) {
+    size_t inner = len >= 4 ? len - 4 : 0;
+    uint8_t st;
+    oracle_frame_digest(f, inner, mtu, 0, d, &st);
+    if (len < 4) {
+        st = FS_ERR_FCS;
+    } else {
+        uint32_t fcs = (uint32_t)f[inner] | ((uint32_t)f[inner + 1] << 8) | ((uint32_t)f[inner + 2] << 16) |
+                       ((uint32_t)f[inner + 3] << 24);
+        if (fcs != d->crc32) st = FS_ERR_FCS;
+    }
+    if (status) *status = st;
+}
+
 typedef struct {
     const uint8_t* frames;
     const uint64_t* offsets;
     const uint32_t* lengths;
     uint32_t begin, end, mtu;
     int use_zlib;
+    int fcs;
     oracle_digest* out;
     uint8_t* status;
 } batch_job;
 
 static void* batch_worker(void* arg) {
     batch_job* j = (batch_job*)arg;
+    if (j->fcs) {
+        for (uint32_t i = j->begin; i < j->end; i++)
+            oracle_frame_digest_fcs(j->frames + j->offsets[i], j->lengths[i], j->mtu, &j->out[i],
+                                    j->status ? &j->status[i] : NULL);
+        return NULL;
+    }
     for (uint32_t i = j->begin; i < j->end; i++)
         oracle_frame_digest(j->frames + j->offsets[i], j->lengths[i], j->mtu, j->use_zlib, &j->out[i],
                             j->status ? &j->status[i] : NULL);
@@ -259,8 +327,8 @@ static void* batch_worker(void* arg) {
 
 /* Batch driver: frame i = frames[offsets[i] : offsets[i] + lengths[i]].
  * `nthreads` > 1 partitions the frames into contiguous blocks (CPU baseline). */
-void oracle_digest_batch(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
-                         uint32_t mtu, int use_zlib, int nthreads, oracle_digest* out, uint8_t* status) {
+static void run_batch(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                      uint32_t mtu, int use_zlib, int fcs, int nthreads, oracle_digest* out, uint8_t* status) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
@@ -273,6 +341,7 @@ void oracle_digest_batch(const uint8_t* frames, const uint64_t* offsets, const u
         jobs[t].end = (uint32_t)(((uint64_t)n * (t + 1)) / nthreads);
         jobs[t].mtu = mtu;
         jobs[t].use_zlib = use_zlib;
+        jobs[t].fcs = fcs;
         jobs[t].out = out;
         jobs[t].status = status;
     }
@@ -282,4 +351,14 @@ void oracle_digest_batch(const uint8_t* frames, const uint64_t* offsets, const u
     }
     for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+void oracle_digest_batch(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                         uint32_t mtu, int use_zlib, int nthreads, oracle_digest* out, uint8_t* status) {
+    run_batch(frames, offsets, lengths, n, mtu, use_zlib, 0, nthreads, out, status);
+}
+
+void oracle_digest_fcs_batch(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                             uint32_t mtu, int nthreads, oracle_digest* out, uint8_t* status) {
+    run_batch(frames, offsets, lengths, n, mtu, 1, 1, nthreads, out, status);
 }

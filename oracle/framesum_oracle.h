@@ -24,8 +24,13 @@ enum {
     FS_ERR_ZERO_PORT = 10,            /* errZeroPort            :129 */
     FS_ERR_BAD_UDP_LENGTH = 11,       /* errBadUDPLength        :133 */
     FS_ERR_BAD_TCP_OFFSET = 12,       /* errBadTCPOffset        :130 */
-    FS_ERR_CHECKSUM = 13              /* ErrChecksumTCPorUDP    :132 */
+    FS_ERR_CHECKSUM = 13,             /* ErrChecksumTCPorUDP    :132 */
+    FS_ERR_FCS = 14                   /* FCS missing or wrong (dropped before RecvEth; not in seqs) */
 };
+
+/* fill flags (TX) */
+#define ORACLE_FILL_CSUM 1u
+#define ORACLE_FCS_APPEND 2u
 
 typedef struct {
     uint32_t crc32;
@@ -55,6 +60,12 @@ uint32_t oracle_crc32_zlib(const uint8_t* p, size_t n);
 uint8_t oracle_recv_eth(const uint8_t* f, size_t len, uint32_t mtu, uint16_t* ip_csum, uint16_t* l4_csum);
 void oracle_frame_digest(const uint8_t* f, size_t len, uint32_t mtu, int use_zlib, oracle_digest* d,
                          uint8_t* status);
+void oracle_fill_frame(uint8_t* f, size_t len, uint32_t mtu, uint32_t flags, oracle_digest* d, uint8_t* status);
+void oracle_fill_batch(uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint32_t mtu,
+                       uint32_t flags, oracle_digest* out, uint8_t* status);
+void oracle_frame_digest_fcs(const uint8_t* f, size_t len, uint32_t mtu, oracle_digest* d, uint8_t* status);
+void oracle_digest_fcs_batch(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                             uint32_t mtu, int nthreads, oracle_digest* out, uint8_t* status);
 void oracle_digest_batch(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, int use_zlib, int nthreads, oracle_digest* out, uint8_t* status);
 

@@ -285,3 +285,37 @@ def frame_digest(frame: bytes, mtu: int = 0) -> tuple[int, int, int, int]:
     """(crc32, ip_csum, l4_csum, verdict) for one frame."""
     verdict, ipc, l4c = recv_eth(frame, mtu)
     return crc32_ieee(frame), ipc, l4c, verdict
+
+
+FS_ERR_FCS = 14  # FCS missing or wrong (dropped before RecvEth; not in the reference)
+FILL_CSUM = 1
+FCS_APPEND = 2
+
+
+def fill_frame(frame: bytes, mtu: int = 0, flags: int = FILL_CSUM) -> tuple[bytes, tuple[int, int, int, int]]:
+    """TX fill of one frame, the struct way: the header checksum fields set as
+    stacks/port_tcp.go:178 + :193 (TCP) and stacks/dhcp_client.go:479 + :486 (UDP) set them,
+    i.e. IPv4 CalculateChecksum() and the L4 checksum RecvEth verifies, for frames that reach
+    its compare. Returns (new bytes incl. the appended FCS if asked, digest of the filled frame)."""
+    f = bytearray(frame)
+    verdict, ipc, got = recv_eth(bytes(f), mtu)
+    if flags & FILL_CSUM and verdict in (FS_OK, FS_ERR_CHECKSUM):
+        ihdr, ip_offset = decode_ipv4_header(bytes(f[14:]))
+        ihdr.checksum = ipc
+        f[14:34] = ihdr.put()  # eth/headers.go:289-301 (version is 4 for any frame that got here)
+        l4 = 14 + ip_offset
+        pos = l4 + (16 if ihdr.protocol == 6 else 6)
+        f[pos : pos + 2] = got.to_bytes(2, "big")
+    dig = frame_digest(bytes(f), mtu)
+    if flags & FCS_APPEND:
+        f += dig[0].to_bytes(4, "little")
+    return bytes(f), dig
+
+
+def frame_digest_fcs(wire: bytes, mtu: int = 0) -> tuple[int, int, int, int]:
+    """(crc32, ip_csum, l4_csum, verdict) of a wire frame carrying its trailing FCS."""
+    inner = wire[:-4] if len(wire) >= 4 else b""
+    crc, ipc, l4c, verdict = frame_digest(inner, mtu)
+    if len(wire) < 4 or int.from_bytes(wire[-4:], "little") != crc:
+        verdict = FS_ERR_FCS
+    return crc, ipc, l4c, verdict

@@ -7,6 +7,9 @@ synthetic-workload generator used by bench.py.
 from .framesum import (  # noqa: F401
     DIGEST_DTYPE,
     EXPORTED_SYMBOLS,
+    FCS_APPEND,
+    FILL_CSUM,
+    FS_ERR_FCS,
     VERDICTS,
     Digest,
     Engine,
@@ -20,6 +23,9 @@ from .framesum import (  # noqa: F401
 __all__ = [
     "DIGEST_DTYPE",
     "EXPORTED_SYMBOLS",
+    "FCS_APPEND",
+    "FILL_CSUM",
+    "FS_ERR_FCS",
     "VERDICTS",
     "Digest",
     "Engine",

@@ -216,6 +216,35 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
     return FS_SUCCESS;
 }
 
+fs_status fs_fill_batch(fs_ctx* ctx, uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                        uint32_t mtu, uint32_t flags, fs_digest* out, uint8_t* status, void* stream) {
+    if (!ctx) return FS_E_INVALID;
+    if (flags & ~(uint32_t)(FS_FILL_CSUM | FS_FCS_APPEND)) return set_err(ctx, FS_E_INVALID, "fs_fill_batch: unknown flags");
+    if (n == 0) return FS_SUCCESS;
+    if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_fill_batch: null pointer");
+    if (reinterpret_cast<uintptr_t>(frames) & 3u)
+        return set_err(ctx, FS_E_INVALID, "fs_fill_batch: frames must be 4-byte aligned");
+    FS_HIP(ctx, hipSetDevice(ctx->device));
+    FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
+                                        reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
+                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFill, frames, flags));
+    return FS_SUCCESS;
+}
+
+fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths,
+                              uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status, void* stream) {
+    if (!ctx) return FS_E_INVALID;
+    if (n == 0) return FS_SUCCESS;
+    if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_fcs: null pointer");
+    if (reinterpret_cast<uintptr_t>(frames) & 3u)
+        return set_err(ctx, FS_E_INVALID, "fs_digest_batch_fcs: frames must be 4-byte aligned");
+    FS_HIP(ctx, hipSetDevice(ctx->device));
+    FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
+                                        reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
+                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFcs));
+    return FS_SUCCESS;
+}
+
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status) {
     if (!ctx) return FS_E_INVALID;

@@ -41,8 +41,13 @@ void build_tables(FsTables* t);
 // that can split long frames into pieces (mode B), others the leaner one-pass variant. The choice never changes a
 // result, only the speed. `force`: 0 = that choice, 1 = always the one-pass kernel, 2 = always
 // the mixed-length kernel (fs_ctx_set_kernel; tests run every case through both).
+// `op`: the RX digest; the TX fill (`wframes` = the same frames, writable; `tx` = FS_FILL_* flags:
+// checksums written into the frames and/or the FCS appended after them); or the RX digest of
+// wire frames whose lengths include a trailing FCS.
+enum class FsOp { kDigest, kFill, kFcs };
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
-                         int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force = 0);
+                         int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force = 0,
+                         FsOp op = FsOp::kDigest, uint8_t* wframes = nullptr, uint32_t tx = 0);
 
 }  // namespace framesum

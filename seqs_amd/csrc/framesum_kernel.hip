@@ -134,8 +134,18 @@ constexpr int kQuadXor2 = 0x4E;  // [2,3,0,1]
 
 enum : uint32_t {
     V_OK = 0, V_SMOL = 1, V_MTU = 2, V_NOT_IPV4 = 3, V_ARP = 4, V_IPVER = 5, V_IHL = 6, V_BADLEN = 7,
-    V_PROTO = 8, V_SHORT = 9, V_ZEROPORT = 10, V_UDPLEN = 11, V_TCPOFF = 12, V_CSUM = 13
+    V_PROTO = 8, V_SHORT = 9, V_ZEROPORT = 10, V_UDPLEN = 11, V_TCPOFF = 12, V_CSUM = 13, V_FCS = 14
 };
+
+// Kernel operations (a template parameter: each is its own instantiation, so the plain digest
+// carries no code of the others).
+//   kOpsDigest : RX digest + verdict (fs_digest_batch)
+//   kOpsTx     : TX fill (fs_fill_batch): the runtime `tx` word's kTxFill writes the IPv4 and L4
+//                checksums into the frame, kTxAppend the FCS after it; the digest is that of
+//                the frame as written
+//   kOpsFcs    : RX of wire frames with a trailing FCS (fs_digest_batch_fcs)
+enum : uint32_t { kOpsDigest = 0, kOpsTx = 1, kOpsFcs = 2 };
+enum : uint32_t { kTxFill = 1, kTxAppend = 2 };
 
 __device__ __forceinline__ uint32_t lds32(const char* lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t*>(lds + byte_addr);
@@ -281,6 +291,7 @@ struct Parsed {
     uint32_t off, end;  // L4 segment [off, end) (frame-relative)
     int64_t corr;       // every checksum correction (16-bit-half domain)
     int64_t corr_fixed; // the pseudo-header and excluded-word part of corr
+    uint32_t aux;       // kOpsTx: stored IPv4 checksum | L4 checksum field offset << 16
 };
 
 // Header parse for one frame (parser lane). Gates follow stacks/portstack.go:163-308
@@ -288,9 +299,10 @@ struct Parsed {
 // compare the two). Reads only the LDS header slot; `hsum` = sum of frame bytes [0, off)
 // and `pad` = sum of the Ethernet padding [end, len), both from the group-vectorised sums
 // (pad < 0: the padding lies past the slot, summed here from global memory).
+template <uint32_t kOps>
 __device__ __forceinline__ Parsed parse_frame(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t len, uint32_t mtu,
                               uint32_t hsum, int64_t pad, const uint32_t* fb) {
-    Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0};
+    Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0, 0u};
     if (len < 34u) { r.verdict = V_SMOL; return r; }                          // portstack.go:167-168
     if (mtu != 0 && len > mtu) { r.verdict = V_MTU; return r; }              // :169-172
     uint32_t bs[9];                                                           // bswap32(frame dword j), j = 3..8
@@ -346,6 +358,7 @@ __device__ __forceinline__ Parsed parse_frame(const char* lds, uint32_t hw, uint
     r.compute = 1;
     r.off = off;
     r.end = end;
+    if (kOps == kOpsTx) r.aux = (bs[6] >> 16) | ((off + (proto == 6u ? 16u : 6u)) << 16);
     // Total over [off, end) = all streamed frame bytes [0, len) + these corrections, in the
     // 16-bit-half domain: a big-endian word at frame offset p (even) weighs 256^((sa + p) & 1),
     // i.e. it enters as itself when the L4 start is odd, byte-swapped when even.
@@ -371,17 +384,22 @@ __device__ __forceinline__ Parsed parse_frame(const char* lds, uint32_t hw, uint
 // The parse result lives in LDS while the rows stream (it would otherwise hold 11 VGPRs
 // across the row loops): dwords 0..10 of the group's header slot, dead after the parse and
 // rewritten only by the next tile's header DMA, after this tile's finish.
+template <uint32_t kOps>
 __device__ __forceinline__ void park_parsed(char* lds, uint32_t hw, uint32_t g, const Parsed& P) {
-    const uint32_t v[11] = {P.verdict, P.ip_csum, P.stored, (uint32_t)P.compute, (uint32_t)P.parity, P.off, P.end,
+    constexpr uint32_t kN = kOps == kOpsTx ? 12 : 11;
+    const uint32_t v[12] = {P.verdict, P.ip_csum, P.stored, (uint32_t)P.compute, (uint32_t)P.parity, P.off, P.end,
                             (uint32_t)P.corr, (uint32_t)((uint64_t)P.corr >> 32), (uint32_t)P.corr_fixed,
-                            (uint32_t)((uint64_t)P.corr_fixed >> 32)};
+                            (uint32_t)((uint64_t)P.corr_fixed >> 32), P.aux};
 #pragma unroll
-    for (uint32_t k = 0; k < 11; ++k) *reinterpret_cast<uint32_t*>(lds + hdr_at(hw, g, k)) = v[k];
+    for (uint32_t k = 0; k < kN; ++k) *reinterpret_cast<uint32_t*>(lds + hdr_at(hw, g, k)) = v[k];
 }
+template <uint32_t kOps>
 __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, uint32_t g) {
-    uint32_t v[11];
+    constexpr uint32_t kN = kOps == kOpsTx ? 12 : 11;
+    uint32_t v[12];
+    v[11] = 0u;
 #pragma unroll
-    for (uint32_t k = 0; k < 11; ++k) v[k] = hdr_dw(lds, hw, g, k);
+    for (uint32_t k = 0; k < kN; ++k) v[k] = hdr_dw(lds, hw, g, k);
     Parsed P;
     P.verdict = v[0];
     P.ip_csum = v[1];
@@ -392,6 +410,7 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, ui
     P.end = v[6];
     P.corr = (int64_t)(((uint64_t)v[8] << 32) | v[7]);
     P.corr_fixed = (int64_t)(((uint64_t)v[10] << 32) | v[9]);
+    P.aux = v[11];
     return P;
 }
 
@@ -400,6 +419,7 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, ui
 // call saves nothing). Every lane takes part: group-vectorised sums over the header slot
 // (the bytes [0, off) of the Ethernet + IP headers; the Ethernet padding [end, len) when it
 // lies in the slot), then the parser lane's gates and corrections, parked in LDS.
+template <uint32_t kOps>
 __device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
                                                      uint32_t mtu, const uint32_t* fbs, bool parser) {
     const char* lds = g_lds;
@@ -415,7 +435,7 @@ __device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, 
         const uint32_t ps = slot_sum(lds, hw, grp, gl, sa, (int)min(end, len), (int)len, kHdrDwords / 4);
         if (pad_in_slot) pad = (int64_t)ps;
     }
-    if (parser) park_parsed(g_lds, hw, grp, parse_frame(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
+    if (parser) park_parsed<kOps>(g_lds, hw, grp, parse_frame<kOps>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
 }
 
 // Final L4 checksum + verdict (parser lane) once the streamed sum is known.
@@ -437,6 +457,84 @@ __device__ uint32_t finish_l4(const uint32_t* fb, uint32_t sa, uint32_t len, con
     if (!P.parity) l4 = bswap16(l4);
     verdict = (l4 == P.stored) ? V_OK : V_CSUM;
     return l4;
+}
+
+// Z_k(v) for any k (one lane, a few uses per frame): Z768 and Z64 steps, then the sub-64
+// tables (Z48/Z32/Z16, Z12/Z8/Z4, Z3/Z2/Z1). Z64 reads region A's copy 0 (entry e, table b:
+// byte e*256 + 32*b).
+__device__ __forceinline__ uint32_t zshift(const char* lds, uint32_t v, uint32_t k) {
+    for (; k >= 768u; k -= 768u) v = zplain(lds, v, kLdsZ768);
+    for (; k >= 64u; k -= 64u)
+        v = lds32(lds, (v & 0xffu) << 8) ^ lds32(lds, (((v >> 8) & 0xffu) << 8) + 32u) ^
+            lds32(lds, (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, ((v >> 24) << 8) + 96u);
+    if (k >= 48u) { v = zplain(lds, v, kLdsZ48); k -= 48u; }
+    else if (k >= 32u) { v = zplain(lds, v, kLdsZ32); k -= 32u; }
+    else if (k >= 16u) { v = zplain(lds, v, kLdsZ16); k -= 16u; }
+    if (k >= 12u) { v = zplain(lds, v, kLdsZ12); k -= 12u; }
+    else if (k >= 8u) { v = zplain(lds, v, kLdsZ8); k -= 8u; }
+    else if (k >= 4u) { v = zplain(lds, v, kLdsZfin); k -= 4u; }
+    if (k > 0u) v = zplain(lds, v, kLdsZfin + 4096u * (4u - k));  // zfin[t] = Z_(4-t)
+    return v;
+}
+
+// The parser lane's finish of one frame: CRC-32 from the combined register Y, L4 checksum and
+// verdict from the streamed sum `cs` and the parked parse, then the op's writes and stores.
+// `len` is the frame length the rows streamed (kOpsFcs: without the FCS).
+template <uint32_t kOps>
+__device__ __forceinline__ void finish_frame(const char* lds, uint32_t hw, uint32_t grp, uint64_t S, uint32_t len,
+                                             uint32_t te, uint32_t Y, uint32_t cs, const uint8_t* frames,
+                                             uint8_t* wframes, const uint32_t* lengths, uint32_t fi, uint2* out,
+                                             uint8_t* status, uint32_t tx) {
+    uint32_t fcs = 0u;
+    if (kOps == kOpsFcs) {  // the FCS bytes [len, len+4): issued first, used last
+        const uint8_t* fp = frames + S + len;
+        fcs = (uint32_t)fp[0] | ((uint32_t)fp[1] << 8) | ((uint32_t)fp[2] << 16) | ((uint32_t)fp[3] << 24);
+    }
+    const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
+    const uint32_t sa = (uint32_t)S & 3u;
+    const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2));
+    uint32_t crcv;
+    if (len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
+        uint32_t c = 0xffffffffu;
+        const uint8_t* fbytes = frames + S;
+        for (uint32_t p = 0; p < len; ++p)
+            c = lds32(lds, kLdsZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
+        crcv = ~c;
+    } else {
+        const uint32_t tpad = (4u - te) & 3u;  // zero bytes appended by the dword rounding
+        crcv = ~zplain(lds, Y, kLdsZfin + 4096u * tpad);
+    }
+    uint32_t verdict = P.verdict, l4 = 0u;
+    if (P.compute) l4 = finish_l4(fbs, sa, len, P, cs, verdict);
+    if (kOps == kOpsTx) {
+        uint8_t* wf = wframes + S;
+        if ((tx & kTxFill) && P.compute) {
+            // write the IPv4 checksum at [24, 26) and the L4 checksum at its field, big-endian;
+            // the CRC of the written frame differs from the streamed one by the CRC (zero init)
+            // of the two 16-bit XOR deltas: Z_(len-p2)( Z_(p2-24)(d_ip) ^ d_l4 ), d as LE bytes
+            const uint32_t ipc = P.ip_csum, old_ip = P.aux & 0xffffu, p2 = P.aux >> 16;
+            const uint32_t d = zshift(lds, bswap16(old_ip ^ ipc), p2 - 24u) ^ bswap16(P.stored ^ l4);
+            crcv ^= zshift(lds, d, len - p2);
+            wf[24] = (uint8_t)(ipc >> 8);
+            wf[25] = (uint8_t)ipc;
+            wf[p2] = (uint8_t)(l4 >> 8);
+            wf[p2 + 1] = (uint8_t)l4;
+            verdict = V_OK;  // the written field now holds the computed checksum
+        }
+        if (tx & kTxAppend) {
+            wf[len] = (uint8_t)crcv;
+            wf[len + 1] = (uint8_t)(crcv >> 8);
+            wf[len + 2] = (uint8_t)(crcv >> 16);
+            wf[len + 3] = (uint8_t)(crcv >> 24);
+        }
+    }
+    if (kOps == kOpsFcs) {
+        // len 0 covers wire frames of 0..4 bytes: only those of 4 carry an FCS
+        const bool present = len > 0u || lengths[fi] >= 4u;
+        if (!present || fcs != crcv) verdict = V_FCS;
+    }
+    out[fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
+    if (status) status[fi] = (uint8_t)verdict;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -505,8 +603,11 @@ __device__ __forceinline__ void tile_descriptors(uint32_t tile, uint32_t grp, ui
 }
 
 // vmcnt(0) tied to the descriptor registers, so no use of them is scheduled above it.
+// kOpsFcs: the rows stream the frame without its trailing FCS.
+template <uint32_t kOps>
 __device__ __forceinline__ void descriptors_ready(uint64_t& S, uint32_t& len) {
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(S), "+v"(len));
+    if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
 }
 
 // Wave max (sum) of a value that is uniform within each 4-lane group: two DPP row mirrors
@@ -847,10 +948,11 @@ __device__ __forceinline__ void post_report(uint64_t report) {
 // The kernel for batches of similar lengths: every tile in mode A (one pass). It reports in
 // `report` whether any tile would have run better in mode B, so that the host launches
 // digest_kernel_ab next time (launch_digest).
+template <uint32_t kOps>
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
                 const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
-                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report) {
+                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx) {
     char* lds = g_lds;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -890,7 +992,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         uint32_t len;
         tile_descriptors(tile, grp, n, offsets, lengths, S, len);
         build_region_a(tabs, lds);
-        descriptors_ready(S, len);
+        descriptors_ready<kOps>(S, len);
         T.P = 0;
         if (first) {
             tile_geometry_a(T, tile, grp, gl, n, S, len, frames);
@@ -932,7 +1034,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         auto parse = [&](bool refilled) {
             if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
             else __builtin_amdgcn_s_waitcnt(0x0070);
-            parse_tile(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
+            parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
                        parser);
         };
         auto prio = [&](int r0) {
@@ -1027,26 +1129,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         cs += dpp_quad<kQuadXor2>(cs);
         FS_STAMP(3);
         // ---- the group's lane 0: finish and store (its frame's parse comes back from LDS).
-        if (parser) {
-            const Parsed P = unpark_parsed(lds, hw, grp);
-            uint32_t crcv;
-            const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2));
-            if (T.len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
-                uint32_t c = 0xffffffffu;
-                const uint8_t* fbytes = frames + T.S;
-                for (uint32_t p = 0; p < T.len; ++p)
-                    c = lds32(lds, kLdsZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
-                crcv = ~c;
-            } else {
-                const uint32_t tpad = (4u - T.te()) & 3u;  // zero bytes appended by the dword rounding
-                crcv = ~zplain(lds, Y, kLdsZfin + 4096u * tpad);
-            }
-            uint32_t verdict = P.verdict, l4 = 0u;
-            if (P.compute) l4 = finish_l4(fbs, T.sa(), T.len, P, cs, verdict);
-            const uint32_t fi = tile * kFramesPerTile + grp;
-            out[fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
-            if (status) status[fi] = (uint8_t)verdict;
-        }
+        if (parser)
+            finish_frame<kOps>(lds, hw, grp, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths,
+                               tile * kFramesPerTile + grp, out, status, tx);
         FS_STAMP(4);
         FS_RTSTAMP(6);
         tile += nwaves;
@@ -1054,7 +1139,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             uint64_t S;
             uint32_t len;
             tile_descriptors(tile, grp, n, offsets, lengths, S, len);
-            descriptors_ready(S, len);
+            descriptors_ready<kOps>(S, len);
             tile_geometry_a(T, tile, grp, gl, n, S, len, frames);
             if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             header_dma(T, frames, lds, hw, gl);
@@ -1070,10 +1155,11 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
 }
 
 // The kernel for batches with mixed lengths: tiles in mode A or mode B, per tile.
+template <uint32_t kOps>
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
                  const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
-                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report) {
+                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx) {
     char* lds = g_lds;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1119,7 +1205,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         uint32_t len;
         tile_descriptors(tile, grp0, n, offsets, lengths, S, len);
         build_region_a(tabs, lds);
-        descriptors_ready(S, len);
+        descriptors_ready<kOps>(S, len);
         U.P = 0;
         if (first) tile_geometry(T, U, tile, grp0, gl0, n, S, len, frames, lds, ws);
     }
@@ -1156,7 +1242,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         auto parse = [&](bool refilled) {
             if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
             else __builtin_amdgcn_s_waitcnt(0x0070);
-            parse_tile(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
+            parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
                        parser);
         };
         uint32_t Y = 0u, csum = 0u;  // the frame's combined register value and sum (mode A)
@@ -1283,24 +1369,8 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
                     csum += sl.y;
                 }
             }
-            const Parsed P = unpark_parsed(lds, hw, grp);
-            const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2));
-            uint32_t crcv;
-            if (T.len < 4u) {  // too short for the 4-byte init trick: bytewise CRC-32
-                uint32_t c = 0xffffffffu;
-                const uint8_t* fbytes = frames + T.S;
-                for (uint32_t p = 0; p < T.len; ++p)
-                    c = lds32(lds, kLdsZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
-                crcv = ~c;
-            } else {
-                const uint32_t tpad = (4u - T.te()) & 3u;  // zero bytes appended by the dword rounding
-                crcv = ~zplain(lds, Y, kLdsZfin + 4096u * tpad);
-            }
-            uint32_t verdict = P.verdict, l4 = 0u;
-            if (P.compute) l4 = finish_l4(fbs, T.sa(), T.len, P, csum, verdict);
-            const uint32_t fi = tile * kFramesPerTile + grp;
-            out[fi] = make_uint2(crcv, P.ip_csum | (l4 << 16));
-            if (status) status[fi] = (uint8_t)verdict;
+            finish_frame<kOps>(lds, hw, grp, T.S, T.len, T.te(), Y, csum, frames, wframes, lengths,
+                               tile * kFramesPerTile + grp, out, status, tx);
         }
         FS_STAMP(4);
         FS_RTSTAMP(6);
@@ -1309,7 +1379,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             uint64_t S;
             uint32_t len;
             tile_descriptors(tile, grp, n, offsets, lengths, S, len);
-            descriptors_ready(S, len);
+            descriptors_ready<kOps>(S, len);
             tile_geometry(T, U, tile, grp, gl, n, S, len, frames, lds, ws);
             header_dma(T, frames, lds, hw, gl);
             prefetch_unit(U, pf);
@@ -1327,7 +1397,8 @@ extern "C" int fs_debug_read_stamps(void* host, size_t bytes) {
 
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
-                         int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force) {
+                         int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force, FsOp op,
+                         uint8_t* wframes, uint32_t tx) {
     if (n == 0) return hipSuccess;
     const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
     uint32_t blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -1351,12 +1422,25 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         mixed = latest != 0u && ((id - latest) & 0xFFFFu) <= kStickyLaunches;
     }
     if (force) mixed = force == 2;
-    if (mixed)
-        hipLaunchKernelGGL(digest_kernel_ab, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu,
-                           tables, reinterpret_cast<uint2*>(out), status, report);
-    else
-        hipLaunchKernelGGL(digest_kernel_a, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu,
-                           tables, reinterpret_cast<uint2*>(out), status, report);
+    uint2* o = reinterpret_cast<uint2*>(out);
+#define FS_LAUNCH(K, OPS)                                                                                   \
+    hipLaunchKernelGGL((K<OPS>), dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
+                       tables, o, status, report, wframes, tx)
+    switch (op) {
+    case FsOp::kDigest:
+        if (mixed) FS_LAUNCH(digest_kernel_ab, kOpsDigest);
+        else FS_LAUNCH(digest_kernel_a, kOpsDigest);
+        break;
+    case FsOp::kFill:
+        if (mixed) FS_LAUNCH(digest_kernel_ab, kOpsTx);
+        else FS_LAUNCH(digest_kernel_a, kOpsTx);
+        break;
+    case FsOp::kFcs:
+        if (mixed) FS_LAUNCH(digest_kernel_ab, kOpsFcs);
+        else FS_LAUNCH(digest_kernel_a, kOpsFcs);
+        break;
+    }
+#undef FS_LAUNCH
     return hipGetLastError();
 }
 

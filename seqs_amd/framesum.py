@@ -45,7 +45,13 @@ VERDICTS = {
     11: "errBadUDPLength",
     12: "errBadTCPOffset",
     13: "ErrChecksumTCPorUDP",
+    14: "FCS missing or wrong (fs_digest_batch_fcs)",
 }
+
+# fs_fill_batch flags
+FILL_CSUM = 1
+FCS_APPEND = 2
+FS_ERR_FCS = 14
 
 # Every symbol include/framesum.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -56,6 +62,8 @@ EXPORTED_SYMBOLS = (
     "fs_last_error",
     "fs_digest_batch",
     "fs_digest_batch_host",
+    "fs_fill_batch",
+    "fs_digest_batch_fcs",
     "fs_ctx_set_kernel",
     "fs_host_alloc",
     "fs_host_free",
@@ -99,6 +107,10 @@ def load_library() -> ctypes.CDLL:
     lib.fs_digest_batch_host.restype = i32
     lib.fs_digest_batch_host.argtypes = [vp, vp, u64, vp, vp, u32, u32, vp, vp]
     lib.fs_ctx_set_kernel.restype = i32
+    lib.fs_fill_batch.argtypes = [vp, vp, vp, vp, u32, u32, u32, vp, vp, vp]
+    lib.fs_fill_batch.restype = ctypes.c_int32
+    lib.fs_digest_batch_fcs.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp]
+    lib.fs_digest_batch_fcs.restype = ctypes.c_int32
     lib.fs_ctx_set_kernel.argtypes = [vp, ctypes.c_int]
     lib.fs_host_alloc.restype = i32
     lib.fs_host_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
@@ -195,6 +207,46 @@ class Engine:
             ctypes.c_void_p(stream.cuda_stream),
         )
         self._check(st, "fs_digest_batch")
+        return out, status
+
+    def _device_args(self, frames, offsets, lengths, out, status, stream):
+        import torch
+
+        n = int(lengths.numel())
+        assert frames.is_cuda and offsets.is_cuda and lengths.is_cuda, "device-resident path needs CUDA tensors"
+        assert frames.dtype == torch.uint8 and offsets.dtype == torch.int64 and lengths.dtype == torch.int32
+        assert offsets.numel() == n and frames.is_contiguous() and offsets.is_contiguous() and lengths.is_contiguous()
+        if out is None:
+            out = torch.empty((n, 2), dtype=torch.int32, device=frames.device)
+        if status is None:
+            status = torch.empty((n,), dtype=torch.uint8, device=frames.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.device)
+        return n, out, status, stream
+
+    def fill_device(self, frames, offsets, lengths, mtu: int = 0, flags: int = FILL_CSUM, out=None, status=None,
+                    stream=None):
+        """TX fill IN PLACE on the device tensor `frames` (fs_fill_batch): FILL_CSUM writes the
+        IPv4 and TCP/UDP checksums into every frame RecvEth would checksum, FCS_APPEND the
+        CRC-32 after each frame (4 spare bytes needed there). Returns (out, status) as
+        digest_device would report them for the written frames."""
+        n, out, status, stream = self._device_args(frames, offsets, lengths, out, status, stream)
+        st = self.lib.fs_fill_batch(
+            self._ctx, ctypes.c_void_p(frames.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
+            ctypes.c_void_p(lengths.data_ptr()), n, mtu, flags, ctypes.c_void_p(out.data_ptr()),
+            ctypes.c_void_p(status.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
+        self._check(st, "fs_fill_batch")
+        return out, status
+
+    def digest_fcs_device(self, frames, offsets, lengths, mtu: int = 0, out=None, status=None, stream=None):
+        """RX digest of wire frames with a trailing FCS (fs_digest_batch_fcs): lengths include
+        the FCS; status FS_ERR_FCS (14) where it is missing or wrong."""
+        n, out, status, stream = self._device_args(frames, offsets, lengths, out, status, stream)
+        st = self.lib.fs_digest_batch_fcs(
+            self._ctx, ctypes.c_void_p(frames.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
+            ctypes.c_void_p(lengths.data_ptr()), n, mtu, ctypes.c_void_p(out.data_ptr()),
+            ctypes.c_void_p(status.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
+        self._check(st, "fs_digest_batch_fcs")
         return out, status
 
     # ---- host-staged path (numpy in, numpy out) -----------------------------

@@ -45,7 +45,7 @@ def test_verdict_codes_match_oracle_header():
     orc = open(os.path.join(ROOT, "oracle", "framesum_oracle.h")).read()
     pat = re.compile(r"(FS_[A-Z0-9_]+)\s*=\s*(\d+)")
     a, b = dict(pat.findall(hdr)), dict(pat.findall(orc))
-    assert a == b and len(a) == 14
+    assert a == b and len(a) == 15
     assert {int(v): k for k, v in a.items()}.keys() == framesum.VERDICTS.keys()
 
 
