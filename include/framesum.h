@@ -129,6 +129,14 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
 fs_status fs_fill_batch(fs_ctx* ctx, uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                         uint32_t mtu, uint32_t flags, fs_digest* out, uint8_t* status, void* stream);
 
+/* fs_fill_batch from/to HOST memory (the TX buffer a stack writes frames into): copies the
+ * batch's byte span to the device, fills, copies the span back into `frames`, and returns
+ * when the frames and `out`/`status` are written. frames_bytes bounds every frame (plus its
+ * 4 FCS bytes with FS_FCS_APPEND). */
+fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
+                             const uint32_t* lengths, uint32_t n, uint32_t mtu, uint32_t flags, fs_digest* out,
+                             uint8_t* status);
+
 /* RX of raw wire frames that still carry their 4-byte FCS (NICs that do not strip it;
  * SURVEY.md §8f rank 4, not in the reference): lengths[i] includes the FCS. out/status are
  * fs_digest_batch's for frame[0:len-4), the bytes RecvEth would receive, except that status

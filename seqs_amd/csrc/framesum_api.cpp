@@ -320,6 +320,61 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     return FS_SUCCESS;
 }
 
+fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
+                             const uint32_t* lengths, uint32_t n, uint32_t mtu, uint32_t flags, fs_digest* out,
+                             uint8_t* status) {
+    if (!ctx) return FS_E_INVALID;
+    if (flags & ~(uint32_t)(FS_FILL_CSUM | FS_FCS_APPEND))
+        return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: unknown flags");
+    if (n == 0) return FS_SUCCESS;
+    if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: null pointer");
+    // One staged span [lo, hi) (the frames and, with FS_FCS_APPEND, their FCS bytes), copied in,
+    // filled, copied back. Not chunk-pipelined: written spans of unordered batches may interleave.
+    const uint64_t extra = (flags & FS_FCS_APPEND) ? 4u : 0u;
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t o = offsets[i], e = o + lengths[i] + extra;
+        if (e > frames_bytes)
+            return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: frame " + std::to_string(i) + " ends past frames_bytes");
+        lo = o < lo ? o : lo;
+        hi = e > hi ? e : hi;
+    }
+    FS_HIP(ctx, hipSetDevice(ctx->device));
+    FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));
+    fs_status pst = ensure_pinned(ctx, n);
+    if (pst != FS_SUCCESS) return pst;
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pin);
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pin + (size_t)n * 8);
+    fs_digest* h_out = reinterpret_cast<fs_digest*>(ctx->h_pin + (size_t)n * 12);
+    uint8_t* h_st = ctx->h_pin + (size_t)n * 20;
+    std::memcpy(h_off, offsets, (size_t)n * 8);
+    std::memcpy(h_len, lengths, (size_t)n * 4);
+    const uint64_t cpy_lo = (lo >= 16 ? lo - 16 : 0) & ~uint64_t(15);
+    uint64_t cpy_hi = (hi + 3) & ~uint64_t(3);
+    if (cpy_hi > frames_bytes) cpy_hi = frames_bytes;
+    HostSlot& sl = ctx->slot[0];
+    fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, n);
+    if (st != FS_SUCCESS) return st;
+    hipStream_t ks = ctx->compute_stream;
+    if (sl.used) FS_HIP(ctx, hipStreamWaitEvent(ks, sl.consumed, 0));
+    FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, ks));
+    FS_HIP(ctx, hipMemcpyAsync(sl.d_offsets, h_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
+    FS_HIP(ctx, hipMemcpyAsync(sl.d_lengths, h_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+    uint8_t* base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
+    FS_HIP(ctx, framesum::launch_digest(base, sl.d_offsets, sl.d_lengths, n, mtu, ctx->d_tables, sl.d_out,
+                                        status ? sl.d_status : nullptr, ks, ctx->num_cus, ctx->h_report,
+                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFill, base, flags));
+    FS_HIP(ctx, hipMemcpyAsync(frames + lo, sl.d_frames + (lo - cpy_lo), hi - lo, hipMemcpyDeviceToHost, ks));
+    FS_HIP(ctx, hipMemcpyAsync(h_out, sl.d_out, (size_t)n * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
+    if (status) FS_HIP(ctx, hipMemcpyAsync(h_st, sl.d_status, n, hipMemcpyDeviceToHost, ks));
+    FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
+    sl.used = true;
+    FS_HIP(ctx, hipStreamSynchronize(ks));
+    std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
+    if (status) std::memcpy(status, h_st, n);
+    return FS_SUCCESS;
+}
+
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
     if (variant < 0 || variant > 2) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0, 1 or 2");

@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "fs_digest_batch",
     "fs_digest_batch_host",
     "fs_fill_batch",
+    "fs_fill_batch_host",
     "fs_digest_batch_fcs",
     "fs_ctx_set_kernel",
     "fs_host_alloc",
@@ -109,6 +110,8 @@ def load_library() -> ctypes.CDLL:
     lib.fs_ctx_set_kernel.restype = i32
     lib.fs_fill_batch.argtypes = [vp, vp, vp, vp, u32, u32, u32, vp, vp, vp]
     lib.fs_fill_batch.restype = ctypes.c_int32
+    lib.fs_fill_batch_host.argtypes = [vp, vp, u64, vp, vp, u32, u32, u32, vp, vp]
+    lib.fs_fill_batch_host.restype = ctypes.c_int32
     lib.fs_digest_batch_fcs.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp]
     lib.fs_digest_batch_fcs.restype = ctypes.c_int32
     lib.fs_ctx_set_kernel.argtypes = [vp, ctypes.c_int]
@@ -302,6 +305,26 @@ class Engine:
         self._check(st, "fs_digest_batch_host")
         return out, status
 
+    def fill_host(self, frames: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, mtu: int = 0,
+                  flags: int = FILL_CSUM):
+        """TX fill IN PLACE on a writable host uint8 array (fs_fill_batch_host). Returns
+        (digests, status) of the frames as written."""
+        assert isinstance(frames, np.ndarray) and frames.dtype == np.uint8 and frames.flags["C_CONTIGUOUS"]
+        assert frames.flags["WRITEABLE"], "fill_host writes into `frames`"
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        n = int(lengths.size)
+        out = np.zeros(n, dtype=DIGEST_DTYPE)
+        status = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return out, status
+        st = self.lib.fs_fill_batch_host(
+            self._ctx, frames.ctypes.data_as(ctypes.c_void_p), frames.nbytes,
+            offsets.ctypes.data_as(ctypes.c_void_p), lengths.ctypes.data_as(ctypes.c_void_p), n, mtu, flags,
+            out.ctypes.data_as(ctypes.c_void_p), status.ctypes.data_as(ctypes.c_void_p))
+        self._check(st, "fs_fill_batch_host")
+        return out, status
+
     # ---- reference-shaped surface -------------------------------------------
     def digest_batch(self, frames: Sequence[bytes], mtu: int = 0) -> list[Digest]:
         """Batched equivalent of RecvEth's checksum work for each frame (host lists)."""
@@ -312,6 +335,17 @@ class Engine:
     def recv_eth_batch(self, frames: Sequence[bytes], mtu: int = 0) -> list[Optional[str]]:
         """Per-frame RecvEth error class (None = checksum OK), like RecvEth's return."""
         return [d.err for d in self.digest_batch(frames, mtu)]
+
+    def calculate_headers_batch(self, frames: Sequence[bytes], mtu: int = 0, append_fcs: bool = False) -> list[bytes]:
+        """The checksum part of the reference's TX header calculation (stacks/port_tcp.go:178,
+        :193; dhcp_client.go:479, :486) for many frames: each frame with its IPv4 and TCP/UDP
+        checksum fields filled (frames RecvEth would not checksum come back unchanged), and
+        with its FCS appended when `append_fcs`."""
+        room = 4 if append_fcs else 0
+        buf, offsets, lengths = pack_frames([bytes(f) + bytes(room) for f in frames])
+        lengths = lengths - np.uint32(room)
+        self.fill_host(buf, offsets, lengths, mtu, FILL_CSUM | (FCS_APPEND if append_fcs else 0))
+        return [bytes(buf[int(o) : int(o) + int(l) + room]) for o, l in zip(offsets, lengths)]
 
 
 def pack_frames(frames: Sequence[bytes], align: int = 4):

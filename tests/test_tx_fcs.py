@@ -237,3 +237,20 @@ def test_gpu_fcs_c3_round_trip(engine):
     gw, gst = gpu_fcs(engine, buf, off, ln)
     edig, est = coracle.digest_fcs_batch(buf, off, ln)
     assert (gst == 0).all() and np.array_equal(gst, est) and np.array_equal(gw, words(edig))
+
+
+@pytest.mark.gpu
+def test_gpu_fill_host_and_calculate_headers(engine):
+    # host-staged fill (fs_fill_batch_host) and the reference-shaped list surface, against the
+    # Python restatement of the TX header calculation
+    frames = tx_frames(7, n_random=200)
+    buf, off, ln = pack_with_room(frames, align=1)
+    ebuf = buf.copy()
+    edig, est = coracle.fill_batch(ebuf, off, ln, 0, FILL_CSUM | FCS_APPEND)
+    dig, st = engine.fill_host(buf, off, ln, 0, FILL_CSUM | FCS_APPEND)
+    assert np.array_equal(buf, ebuf) and np.array_equal(dig, edig) and np.array_equal(st, est)
+    got = engine.calculate_headers_batch(frames, append_fcs=True)
+    for f, g in zip(frames, got):
+        assert g == pyref.fill_frame(f, 0, FILL_CSUM | FCS_APPEND)[0]
+    with pytest.raises(Exception):
+        engine.fill_host(np.zeros(100, np.uint8), np.array([90], np.uint64), np.array([8], np.uint32), 0, FCS_APPEND)
