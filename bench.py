@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
     p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather (N>1 diagnostics)")
+    p.add_argument("--op", choices=["digest", "fill", "fcs"], default="digest",
+                   help="digest: RX digest + verdict (the BASELINE metric); fill: TX checksum fill + FCS "
+                        "append in place (fs_fill_batch); fcs: RX of wire frames carrying an FCS")
     p.add_argument("--streams", type=int, default=2,
                    help="HIP streams the steps rotate over: step i+1's kernel starts on the CUs step i's "
                         "tail frees (every batch is still fully digested)")
@@ -55,6 +58,17 @@ def make_batch(cfg: str, n: int, seed: int):
     if cfg == "c2":
         return synth.uniform_batch(n, 1500, seed=seed)
     return synth.mixed_batch(n, seed=seed)
+
+
+def with_room(buf, off, ln, room: int = 4):
+    """Repack a batch with `room` spare bytes after every frame (FCS space), 4-byte aligned."""
+    step = (ln.astype(np.int64) + room + 3) // 4 * 4
+    noff = np.zeros_like(off)
+    noff[1:] = np.cumsum(step[:-1])
+    nbuf = np.zeros(int(noff[-1] + step[-1]) + 16, np.uint8)
+    for o, no, l in zip(off, noff, ln):
+        nbuf[no : no + l] = buf[o : o + l]
+    return nbuf, noff, ln
 
 
 def cpu_model() -> str:
@@ -133,9 +147,16 @@ def main():
     batches = []
     for b in range(max(1, args.batches)):
         buf, off, ln = make_batch(args.config, n, seed=1 + 1000 * rank + b)
-        batches.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev),
-                        torch.from_numpy(ln).to(dev)))
-    bytes_per_batch = int(ln.astype(np.int64).sum())
+        if args.op != "digest":
+            buf, off, ln = with_room(buf, off, ln)
+        tb, to, tl = torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)
+        if args.op == "fcs":  # wire frames: the FCS appended once on the GPU, lengths include it
+            engine.fill_device(tb, to, tl, flags=2)
+            tl = tl + 4
+        batches.append((tb, to, tl))
+    run_op = {"digest": engine.digest_device, "fcs": engine.digest_fcs_device,
+              "fill": lambda *a, **k: engine.fill_device(*a, flags=3, **k)}[args.op]
+    bytes_per_batch = int(batches[-1][2].cpu().numpy().astype(np.int64).sum())
     resident = sum(int(x[0].numel()) for x in batches)
     nb = len(batches)
     ns = max(1, args.streams)
@@ -159,7 +180,7 @@ def main():
                 s.wait_event(slot_done[k])
             if ev is not None:
                 ev[0].record(s)
-            engine.digest_device(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=s)
+            run_op(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=s)
             if ev is not None:
                 ev[1].record(s)
             if gather:
@@ -208,7 +229,7 @@ def main():
         k0.record(main_stream)
         for i in range(args.steps):  # same stream, in order: no slot events needed
             fb, fo, fl = batches[i % nb]
-            engine.digest_device(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=main_stream)
+            run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=main_stream)
         k1.record(main_stream)
     torch.cuda.synchronize()
     k_avg_ms = k0.elapsed_time(k1) / args.steps
@@ -216,12 +237,12 @@ def main():
     total_bytes = bytes_per_batch * args.steps * world
     value = total_bytes / elapsed / GIB
     achieved_gbs = bytes_per_batch / (k_avg_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(args.config)
+    traffic = load_pmc_traffic(args.config) if args.op == "digest" else None
 
     result = None
     if rank == 0:
         cpu = None
-        if world == 1 and args.cpu_seconds > 0:
+        if world == 1 and args.cpu_seconds > 0 and args.op == "digest":
             cpu = cpu_baseline(args.config, args.cpu_seconds, args.cpu_threads)
         result = {
             "metric": "GiB/s device-resident CRC-32+Internet-csum over batched MTU frames; % HBM peak",
@@ -246,6 +267,9 @@ def main():
                 "parallelism": f"frames sharded round-robin over {world} GPU(s); RCCL gather of digests to rank 0"
                 if world > 1 else "single GPU",
                 "streams": ns,
+                "op": {"digest": "RX digest + verdict (fs_digest_batch)",
+                       "fill": "TX checksum fill + FCS append in place (fs_fill_batch, 4 spare bytes per frame)",
+                       "fcs": "RX of wire frames with FCS (fs_digest_batch_fcs; bytes = frames incl. FCS)"}[args.op],
             },
             "roofline": {
                 "bound": "hbm",

@@ -57,6 +57,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_PREFETCH
 #define FS_PREFETCH 6
 #endif
+#ifndef FS_TXDIAG
+#define FS_TXDIAG 0  // diagnostic builds only: 1 skips the fill's CRC correction, 2 its field stores, 4 the FCS stores
+#endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio per block of rows
 #endif
@@ -477,6 +480,10 @@ __device__ __forceinline__ uint32_t zshift(const char* lds, uint32_t v, uint32_t
     return v;
 }
 
+// A byte store into a frame (TX; hipcc merges neighbours into short/dword stores). Non-temporal
+// stores measured no faster: the cost of these writes is the dirty lines' write-back.
+__device__ __forceinline__ void st8(uint8_t* p, uint32_t v) { *p = (uint8_t)v; }
+
 // The parser lane's finish of one frame: CRC-32 from the combined register Y, L4 checksum and
 // verdict from the streamed sum `cs` and the parked parse, then the op's writes and stores.
 // `len` is the frame length the rows streamed (kOpsFcs: without the FCS).
@@ -513,19 +520,23 @@ __device__ __forceinline__ void finish_frame(const char* lds, uint32_t hw, uint3
             // the CRC of the written frame differs from the streamed one by the CRC (zero init)
             // of the two 16-bit XOR deltas: Z_(len-p2)( Z_(p2-24)(d_ip) ^ d_l4 ), d as LE bytes
             const uint32_t ipc = P.ip_csum, old_ip = P.aux & 0xffffu, p2 = P.aux >> 16;
-            const uint32_t d = zshift(lds, bswap16(old_ip ^ ipc), p2 - 24u) ^ bswap16(P.stored ^ l4);
-            crcv ^= zshift(lds, d, len - p2);
-            wf[24] = (uint8_t)(ipc >> 8);
-            wf[25] = (uint8_t)ipc;
-            wf[p2] = (uint8_t)(l4 >> 8);
-            wf[p2 + 1] = (uint8_t)l4;
+            if (!(FS_TXDIAG & 1)) {
+                const uint32_t d = zshift(lds, bswap16(old_ip ^ ipc), p2 - 24u) ^ bswap16(P.stored ^ l4);
+                crcv ^= zshift(lds, d, len - p2);
+            }
+            if (!(FS_TXDIAG & 2)) {
+                st8(wf + 24, ipc >> 8);
+                st8(wf + 25, ipc);
+                st8(wf + p2, l4 >> 8);
+                st8(wf + p2 + 1, l4);
+            }
             verdict = V_OK;  // the written field now holds the computed checksum
         }
-        if (tx & kTxAppend) {
-            wf[len] = (uint8_t)crcv;
-            wf[len + 1] = (uint8_t)(crcv >> 8);
-            wf[len + 2] = (uint8_t)(crcv >> 16);
-            wf[len + 3] = (uint8_t)(crcv >> 24);
+        if ((tx & kTxAppend) && !(FS_TXDIAG & 4)) {
+            st8(wf + len, crcv);
+            st8(wf + len + 1, crcv >> 8);
+            st8(wf + len + 2, crcv >> 16);
+            st8(wf + len + 3, crcv >> 24);
         }
     }
     if (kOps == kOpsFcs) {
