@@ -60,6 +60,15 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_TXDIAG
 #define FS_TXDIAG 0  // diagnostic builds only: 1 skips the fill's CRC correction, 2 its field stores, 4 the FCS stores
 #endif
+#ifndef FS_DIAG
+#define FS_DIAG 0  // diagnostic builds only (wrong results): 1 no header DMA, 2 no plain-table DMA
+#endif
+#ifndef FS_AGE_PRIO
+#define FS_AGE_PRIO 1  // one-pass kernel: a SIMD's later-started waves get the higher issue priority
+#endif
+#ifndef FS_PRE_PRIO
+#define FS_PRE_PRIO 0  // s_setprio(3) through the preamble (one-pass kernel)
+#endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio per block of rows
 #endif
@@ -906,7 +915,7 @@ __device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, con
     const uint32_t lds0 = lds_base(lds);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
-    for (uint32_t k = 0; k < kDmaPerWave; ++k) {
+    for (uint32_t k = 0; k < ((FS_DIAG & 2) ? 0 : kDmaPerWave); ++k) {
         const uint32_t c = kPlainChunk0 + min(w0 + k * kWavesPerBlock, kPlainChunks - 1u);
         dma_x4(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
                __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
@@ -916,17 +925,52 @@ __device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, con
 // The tile's header slots: 8 dword DMAs; instruction i writes frame dword x = 4i + gl of
 // every group (lane-linear: LDS byte hw + 256 i + 4 lane). Sources are clamped to the
 // frame's last dword (never past it).
-template <class TileT>
-__device__ __forceinline__ void header_dma(const TileT& T, const uint8_t* __restrict__ frames, const char* lds,
-                                           uint32_t hw, uint32_t gl) {
+// When every frame of the tile spans the whole slot (>= 32 dwords), 2 dwordx4 DMAs do it
+// instead: lane L = g + 16 q loads frame dwords [4c, 4c + 4), c = q + 4 k, of group g's frame
+// (instruction k; lane-linear 16 B per lane: the same [x >> 2][group][x & 3] layout). The
+// tile start is VMEM-issue-bound (16 waves' descriptor, header, table and row loads through
+// one CU), so 6 fewer instructions per wave start the row loops earlier.
+// Returns whether the dwordx4 form was used (wave-uniform: 2 instructions, else 8). kX4 = false
+// (the mixed-length kernel: its tiles hold short frames, and the permutes cost it registers)
+// always takes the dword form.
+template <bool kX4, class TileT>
+__device__ __forceinline__ bool header_dma(const TileT& T, const uint8_t* __restrict__ frames, const char* lds,
+                                           uint32_t hw, uint32_t gl, uint32_t lane) {
+    if (FS_DIAG & 1) return false;
     const uint32_t hdr0 = __builtin_amdgcn_readfirstlane(lds_base(lds) + hw);
     const int last = T.ndall() - 1;
     const bool own = T.len > 0u;
-    const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2));
+    const uint64_t fa = reinterpret_cast<uint64_t>(frames + (T.sdw() << 2));
+    if (kX4 && __ballot(own && last < kHdrDwords - 1) == 0) {
+        const int src = (int)((lane & 15u) << 4);  // group (lane & 15)'s lane 0
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)fa);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(fa >> 32));
+        const uint32_t lg = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)T.len);
+        const uint32_t* fb = reinterpret_cast<const uint32_t*>(((uint64_t)hi << 32) | lo);
+        const uint32_t q = lane >> 4;
+        if (lg > 0u) {
+            dma_x4(fb + 4u * q, hdr0);
+            dma_x4(fb + 4u * (q + 4u), hdr0 + 1024u);
+        }
+        return true;
+    }
     if (own) {  // exec-masked: a group with no frame bytes writes nothing (its slot is never used)
+        const uint32_t* fbs = reinterpret_cast<const uint32_t*>(fa);
 #pragma unroll
         for (int i = 0; i < kHdrDmas; ++i) dma_x1(fbs + min(4 * i + (int)gl, last), hdr0 + 256u * i);
     }
+    return false;
+}
+
+// The preamble's wait: the table pieces (issued before the header DMA and the rows) have
+// landed -- vmcnt(rows + header DMAs) -- and lgkmcnt(0): this wave's region-A stores.
+// s_waitcnt field layout (gfx9): vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4], lgkmcnt[11:8]
+__device__ __forceinline__ void tables_landed(bool first, bool rows, bool x4) {
+    if (first && rows && x4) __builtin_amdgcn_s_waitcnt(0x0070 | (kPrefetch + 2));
+    else if (first && rows) __builtin_amdgcn_s_waitcnt(0x0070 | (kPrefetch + kHdrDmas));
+    else if (first && x4) __builtin_amdgcn_s_waitcnt(0x0070 | 2);
+    else if (first) __builtin_amdgcn_s_waitcnt(0x0070 | kHdrDmas);
+    else __builtin_amdgcn_s_waitcnt(0x0070);
 }
 
 // 16-stream combine of a group's piece: U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3 per lane (minus the
@@ -1001,9 +1045,12 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     {
         uint64_t S;
         uint32_t len;
+        if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(3);  // the preamble outranks other waves' row loops
         tile_descriptors(tile, grp, n, offsets, lengths, S, len);
         build_region_a(tabs, lds);
+        FS_STAMP(7);
         descriptors_ready<kOps>(S, len);
+        FS_STAMP(8);
         T.P = 0;
         if (first) {
             tile_geometry_a(T, tile, grp, gl, n, S, len, frames);
@@ -1011,25 +1058,26 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         }
     }
     plain_dma(tabs, lds, wave, lane);
-    if (first) {
-        header_dma(T, frames, lds, hw, gl);
-        if (T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
+    bool x4 = false;
+    if (first) x4 = header_dma<true>(T, frames, lds, hw, gl, lane);
+    if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-            for (int i = 0; i < kPrefetch; ++i) {
-                const int rel = T.rel0 + kRowDwords * i;
-                pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
-            }
+        for (int i = 0; i < kPrefetch; ++i) {
+            const int rel = T.rel0 + kRowDwords * i;
+            pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
         }
     }
     FS_STAMP(9);
-    // the table pieces are older than the header DMA and the rows: vmcnt(header + rows);
-    // lgkmcnt(0): this wave's region-A stores
-    // s_waitcnt field layout (gfx9): vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4], lgkmcnt[11:8]
-    if (first && T.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | (kPrefetch + kHdrDmas));
-    else if (first) __builtin_amdgcn_s_waitcnt(0x0070 | kHdrDmas);
-    else __builtin_amdgcn_s_waitcnt(0x0070);
+    tables_landed(first, T.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (FS_AGE_PRIO) {  // the SIMD's younger waves (wave >> 2: its 4 waves in launch order) outrank the older
+        const uint32_t w = __builtin_amdgcn_readfirstlane(wave) >> 2;
+        if (w == 3u) __builtin_amdgcn_s_setprio(3);
+        else if (w == 2u) __builtin_amdgcn_s_setprio(2);
+        else if (w == 1u) __builtin_amdgcn_s_setprio(1);
+    }
     FS_STAMP(1);
 
     while (tile < ntiles) {
@@ -1153,7 +1201,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             descriptors_ready<kOps>(S, len);
             tile_geometry_a(T, tile, grp, gl, n, S, len, frames);
             if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
-            header_dma(T, frames, lds, hw, gl);
+            header_dma<true>(T, frames, lds, hw, gl, lane);
             if (T.P > 0) {
 #pragma unroll
                 for (int i = 0; i < kPrefetch; ++i) {
@@ -1221,17 +1269,11 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         if (first) tile_geometry(T, U, tile, grp0, gl0, n, S, len, frames, lds, ws);
     }
     plain_dma(tabs, lds, wave, lane);
-    if (first) {
-        header_dma(T, frames, lds, hw, gl0);
-        prefetch_unit(U, pf);
-    }
+    bool x4 = false;
+    if (first) x4 = header_dma<false>(T, frames, lds, hw, gl0, lane);
+    if (first) prefetch_unit(U, pf);
     FS_STAMP(9);
-    // the table pieces are older than the header DMA and the rows: vmcnt(header + rows);
-    // lgkmcnt(0): this wave's region-A stores
-    // s_waitcnt field layout (gfx9): vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4], lgkmcnt[11:8]
-    if (first && U.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | (kPrefetch + kHdrDmas));
-    else if (first) __builtin_amdgcn_s_waitcnt(0x0070 | kHdrDmas);
-    else __builtin_amdgcn_s_waitcnt(0x0070);
+    tables_landed(first, U.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     FS_STAMP(1);
@@ -1392,7 +1434,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             tile_descriptors(tile, grp, n, offsets, lengths, S, len);
             descriptors_ready<kOps>(S, len);
             tile_geometry(T, U, tile, grp, gl, n, S, len, frames, lds, ws);
-            header_dma(T, frames, lds, hw, gl);
+            header_dma<false>(T, frames, lds, hw, gl, lane);
             prefetch_unit(U, pf);
         }
     }

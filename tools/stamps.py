@@ -57,11 +57,16 @@ print(f"  realtime: span {us(re_.max() - t0):.2f} us; wave start offset p50/p90/
       f"{us(np.percentile(re_ - t0, 90)):.2f}/{us((re_ - t0).max()):.2f} us")
 print(f"  memtime ticks per us (median over waves): {np.median((s[:, 4] - s[:, 0]) / np.maximum(1, us(re_ - rs))):.0f}")
 if s[:, 9].any():
-    for nm, a_, b_ in (("start->desc (fine)", 0, 8), ("desc->geom+issue", 8, 9), ("start->geom+issue", 0, 9),
+    for nm, a_, b_ in (("start->regionA", 0, 7), ("regionA->desc", 7, 8), ("start->desc (fine)", 0, 8), ("desc->geom+issue", 8, 9), ("start->geom+issue", 0, 9),
                        ("issue->waitcnt", 9, 10), ("waitcnt->barrier", 10, 1)):
         if s[:, b_].any() and s[:, a_].any():
             d = s[:, b_] - s[:, a_]
             print(f"  {nm:18s} median {int(np.median(d)):8d}  p10 {int(np.percentile(d, 10)):8d}  p90 {int(np.percentile(d, 90)):8d}")
+wib = np.arange(nw) % 16
+for nm, a_, b_ in (("start->desc", 0, 8), ("start->issue", 0, 9), ("barrier wait", 10, 1)):
+    if s[:, b_].any():
+        d = s[:, b_] - s[:, a_]
+        print(f"  {nm} median by wave-in-block:", [int(np.median(d[wib == w])) for w in range(16)])
 # active-wave profile over the launch (realtime, 1-us bins) and the phase boundaries' spread
 span = us(re_.max() - t0)
 bins = np.arange(0, span + 1.0, 1.0)
