@@ -78,7 +78,11 @@ constexpr int kWavesPerBlock = 16;
 constexpr int kThreads = kWave * kWavesPerBlock;
 constexpr int kFramesPerTile = 16;
 constexpr int kRowDwords = 16;
-constexpr int kPrefetch = FS_PREFETCH;
+constexpr int kPrefetch = FS_PREFETCH;  // the mixed-length kernel's ring (a divisor of kPieceRows)
+#ifndef FS_PREFETCH_A
+#define FS_PREFETCH_A 6
+#endif
+constexpr int kPrefetchA = FS_PREFETCH_A;  // the one-pass kernel's ring
 
 // Header slots: frame dwords [0, 32) of each group's frame, written by 8 dword LDS-DMA
 // instructions per wave in the layout [x >> 2][group][x & 3] (256 B per instruction),
@@ -216,6 +220,11 @@ __device__ __forceinline__ uint32_t range_mask(int k, int a0, int a1) {
 
 // A lean row: four Z64 steps and four v_sad_u16, no masks.
 __device__ __forceinline__ void lean_row(const char* lds, const LaneKeys& k, u32x4 v, uint32_t (&A)[4], uint32_t& cs) {
+    if (FS_DIAG & 4) {  // diagnostic: no table lookups (wrong CRC; the loads and the sum stay)
+        A[0] = xor3(A[0], v.x, A[1]); A[1] ^= v.y; A[2] ^= v.z; A[3] ^= v.w;
+        cs = sad16(v.x, cs); cs = sad16(v.y, cs); cs = sad16(v.z, cs); cs = sad16(v.w, cs);
+        return;
+    }
     A[0] = zrep(lds, A[0], k, v.x);
     A[1] = zrep(lds, A[1], k, v.y);
     A[2] = zrep(lds, A[2], k, v.z);
@@ -810,7 +819,7 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     const int nd = T.nd();
     const int rows = (nd + kRowDwords - 1) / kRowDwords;
     const int R = group_max(rows);
-    T.P = (R + kPrefetch - 1) / kPrefetch * kPrefetch;
+    T.P = (R + kPrefetchA - 1) / kPrefetchA * kPrefetchA;
     uint64_t ld_sdw = T.sdw();
     int ld_nd = nd;
     {
@@ -965,9 +974,10 @@ __device__ __forceinline__ bool header_dma(const TileT& T, const uint8_t* __rest
 // The preamble's wait: the table pieces (issued before the header DMA and the rows) have
 // landed -- vmcnt(rows + header DMAs) -- and lgkmcnt(0): this wave's region-A stores.
 // s_waitcnt field layout (gfx9): vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4], lgkmcnt[11:8]
+template <int kPf>
 __device__ __forceinline__ void tables_landed(bool first, bool rows, bool x4) {
-    if (first && rows && x4) __builtin_amdgcn_s_waitcnt(0x0070 | (kPrefetch + 2));
-    else if (first && rows) __builtin_amdgcn_s_waitcnt(0x0070 | (kPrefetch + kHdrDmas));
+    if (first && rows && x4) __builtin_amdgcn_s_waitcnt(0x0070 | (kPf + 2));
+    else if (first && rows) __builtin_amdgcn_s_waitcnt(0x0070 | (kPf + kHdrDmas));
     else if (first && x4) __builtin_amdgcn_s_waitcnt(0x0070 | 2);
     else if (first) __builtin_amdgcn_s_waitcnt(0x0070 | kHdrDmas);
     else __builtin_amdgcn_s_waitcnt(0x0070);
@@ -1040,7 +1050,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     FS_RTSTAMP(5);
     FS_STAMP(0);
     TileA T;
-    u32x4 pf[kPrefetch];
+    u32x4 pf[kPrefetchA];
     const bool first = __builtin_amdgcn_readfirstlane(tile) < ntiles;
     {
         uint64_t S;
@@ -1062,13 +1072,13 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     if (first) x4 = header_dma<true>(T, frames, lds, hw, gl, lane);
     if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-        for (int i = 0; i < kPrefetch; ++i) {
+        for (int i = 0; i < kPrefetchA; ++i) {
             const int rel = T.rel0 + kRowDwords * i;
             pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
         }
     }
     FS_STAMP(9);
-    tables_landed(first, T.P > 0, x4);
+    tables_landed<kPrefetchA>(first, T.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -1088,10 +1098,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
 
         // ---- header parse: after the first block of rows, while the ring's loads are in flight.
-        // The header DMA was issued before the tile's rows; vmcnt(kPrefetch) retires it once the
+        // The header DMA was issued before the tile's rows; vmcnt(kPrefetchA) retires it once the
         // first block's refills are the only younger loads.
         auto parse = [&](bool refilled) {
-            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
+            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetchA);
             else __builtin_amdgcn_s_waitcnt(0x0070);
             parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
                        parser);
@@ -1113,16 +1123,16 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             constexpr bool kRefill = decltype(refill_tag)::value;
             prio(r0);
 #pragma unroll
-            for (int i = 0; i < kPrefetch; ++i) {
+            for (int i = 0; i < kPrefetchA; ++i) {
                 const int r = r0 + i;
                 const int rel = T.rel0 + kRowDwords * r;
                 // consume the ring slot, then refill the SAME registers: no copy of an
-                // in-flight load, so the compiler keeps kPrefetch-1 loads outstanding
+                // in-flight load, so the compiler keeps kPrefetchA-1 loads outstanding
                 if (r < T.H) masked_row(lds, keys, pf[i], rel, load_pos(rel, T.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
                 else lean_row(lds, keys, pf[i], A, cs);
                 if (kRefill) {
-                    const int rn = rel + kRowDwords * kPrefetch;
-                    pf[i] = load_row(T.gfb, r + kPrefetch < T.H ? load_pos(rn, T.lo) : rn);
+                    const int rn = rel + kRowDwords * kPrefetchA;
+                    pf[i] = load_row(T.gfb, r + kPrefetchA < T.H ? load_pos(rn, T.lo) : rn);
                 }
             }
         };
@@ -1131,9 +1141,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         auto lean_block = [&](int r0, auto refill_tag) {
             constexpr bool kRefill = decltype(refill_tag)::value;
             prio(r0);
-            const uint32_t* pb = T.gfb + (T.rel0 + kRowDwords * (r0 + kPrefetch));
+            const uint32_t* pb = T.gfb + (T.rel0 + kRowDwords * (r0 + kPrefetchA));
 #pragma unroll
-            for (int i = 0; i < kPrefetch; ++i) {
+            for (int i = 0; i < kPrefetchA; ++i) {
                 lean_row(lds, keys, pf[i], A, cs);
                 if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
                 // keep consume/refill interleaved per row: unfenced, the scheduler sinks all
@@ -1143,16 +1153,16 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         };
         using Yes = std::true_type;
         using No = std::false_type;
-        const int Rc = T.P - kPrefetch;  // first row of the last block
+        const int Rc = T.P - kPrefetchA;  // first row of the last block
         if (T.P > 0) {
             // [first block] parse [head blocks: general] [body: lean] [last block: no refill]
             if (Rc > 0) {
                 if (T.H > 0) block(0, Yes());
                 else lean_block(0, Yes());
                 parse(true);
-                int r0 = kPrefetch;
-                for (; r0 < Rc && r0 < T.H; r0 += kPrefetch) block(r0, Yes());
-                for (; r0 < Rc; r0 += kPrefetch) lean_block(r0, Yes());
+                int r0 = kPrefetchA;
+                for (; r0 < Rc && r0 < T.H; r0 += kPrefetchA) block(r0, Yes());
+                for (; r0 < Rc; r0 += kPrefetchA) lean_block(r0, Yes());
                 if (Rc < T.H) block(Rc, No());
                 else lean_block(Rc, No());
             } else {
@@ -1172,7 +1182,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         // that junk itself (the last dword enters the combine unshifted) and their sum is
         // sad16 of it: remove both.
         uint32_t junk = 0u;
-        if (T.P > 0 && T.H < T.P && gl == 3u && T.nd() > 0) junk = pf[kPrefetch - 1].w & ~T.tail_mask();
+        if (T.P > 0 && T.H < T.P && gl == 3u && T.nd() > 0) junk = pf[kPrefetchA - 1].w & ~T.tail_mask();
         const uint32_t U =
             zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3] ^ junk;
         cs -= sad16(junk, 0u);
@@ -1204,7 +1214,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             header_dma<true>(T, frames, lds, hw, gl, lane);
             if (T.P > 0) {
 #pragma unroll
-                for (int i = 0; i < kPrefetch; ++i) {
+                for (int i = 0; i < kPrefetchA; ++i) {
                     const int rel = T.rel0 + kRowDwords * i;
                     pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
                 }
@@ -1273,7 +1283,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     if (first) x4 = header_dma<false>(T, frames, lds, hw, gl0, lane);
     if (first) prefetch_unit(U, pf);
     FS_STAMP(9);
-    tables_landed(first, U.P > 0, x4);
+    tables_landed<kPrefetch>(first, U.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     FS_STAMP(1);
