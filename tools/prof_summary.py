@@ -97,6 +97,12 @@ def main():
             out["hbm_bytes_per_launch"] = int(round((2 * med["FETCH_SIZE"] + med.get("WRITE_SIZE", 0.0)) * 1024))
             out["hbm_bytes_note"] = ("(2*FETCH_SIZE + WRITE_SIZE) * 1024: counters in KiB, FETCH_SIZE doubled per the "
                                      "gfx950 correction for wide coalesced reads; separate --pmc passes")
+        cal = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "fetch_size_calibration.json")
+        if "hbm_bytes_per_launch" in out and os.path.exists(cal):
+            f = json.load(open(cal))["pattern_factor"]
+            out["hbm_bytes_per_launch_calibrated"] = int(round(out["hbm_bytes_per_launch"] / f))
+            out["calibration_note"] = (f"divided by {f}: the doubled FETCH_SIZE of this access pattern without "
+                                       "compute over its true bytes (profiles/fetch_size_calibration.json)")
         if "TCC_HIT_sum" in med and "TCC_MISS_sum" in med:
             out["l2_hit_rate"] = med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"])
         with open(os.path.join(dst, f"pmc_{cfg}.json"), "w") as f:
