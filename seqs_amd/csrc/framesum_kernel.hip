@@ -181,6 +181,11 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 // Z64(a) ^ w from replicated region A. Conflict-free.
 __device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const LaneKeys& k, uint32_t w) {
+    if (FS_DIAG & 8) {  // diagnostic: the address VALU without the LDS reads (wrong CRC)
+        const uint32_t u0 = __builtin_amdgcn_perm(a, k.cvec, k.sel[0]), u1 = __builtin_amdgcn_perm(a, k.cvec, k.sel[1]);
+        const uint32_t u2 = __builtin_amdgcn_perm(a, k.cvec, k.sel[2]), u3 = __builtin_amdgcn_perm(a, k.cvec, k.sel[3]);
+        return xor3(xor3(u0, u1, u2), u3, w);
+    }
     uint32_t t0 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
     uint32_t t1 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
     uint32_t t2 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
