@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--op", choices=["digest", "fill", "fcs"], default="digest",
                    help="digest: RX digest + verdict (the BASELINE metric); fill: TX checksum fill + FCS "
                         "append in place (fs_fill_batch); fcs: RX of wire frames carrying an FCS")
-    p.add_argument("--streams", type=int, default=2,
+    p.add_argument("--streams", type=int, default=4,
                    help="HIP streams the steps rotate over: step i+1's kernel starts on the CUs step i's "
                         "tail frees (every batch is still fully digested)")
     return p.parse_args()
@@ -174,25 +174,25 @@ def main():
 
     pending = []
 
-    def step(i: int, ev=None, stream=None):
+    def step(i: int):
         fb, fo, fl = batches[i % nb]
         k = i % nslot
-        s = stream if stream is not None else streams[i % ns]
+        s = streams[i % ns]
+        if not gather:
+            # slot k is only ever written by stream k (nslot == ns for ns >= 2; one stream for
+            # ns == 1): stream order alone keeps a slot's launches apart, no events needed
+            run_op(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=s)
+            return
         with torch.cuda.stream(s):
             if slot_done[k] is not None:
                 s.wait_event(slot_done[k])
-            if ev is not None:
-                ev[0].record(s)
             run_op(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=s)
-            if ev is not None:
-                ev[1].record(s)
-            if gather:
-                # digests of step i go to rank 0 over RCCL while later steps' kernels run;
-                # at most `nslot` gathers are pending (each slot is reused nslot steps later)
-                while len(pending) >= nslot:
-                    pending.pop(0)()
-                _, finish = shard.gather_digests(outs[k], stats[k], world, rank, n * world, async_op=True)
-                pending.append(finish)
+            # digests of step i go to rank 0 over RCCL while later steps' kernels run;
+            # at most `nslot` gathers are pending (each slot is reused nslot steps later)
+            while len(pending) >= nslot:
+                pending.pop(0)()
+            _, finish = shard.gather_digests(outs[k], stats[k], world, rank, n * world, async_op=True)
+            pending.append(finish)
             done = torch.cuda.Event()
             done.record(s)
             slot_done[k] = done
