@@ -35,8 +35,10 @@ GIB = float(1 << 30)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=1000,
+                   help="untimed launches first: throughput reaches its steady state only after several hundred "
+                        "back-to-back launches (with 20 the timed steps measured 5-10%% lower)")
     p.add_argument("--config", choices=["c2", "c3"], default="c2")
     p.add_argument("--frames", type=int, default=65536, help="frames per GPU per step")
     p.add_argument("--batches", type=int, default=4, help="distinct resident batches rotated")
