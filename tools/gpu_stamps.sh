@@ -1,8 +1,9 @@
 #!/bin/bash
+# stamps for given stamp-build variants: tools/gpu_stamps2.sh v2st v3st
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for v in st4 st4f; do
+for v in "$@"; do
   for cfg in c2; do
     echo "== $v $cfg"
     FRAMESUM_LIB="$GRAFT_REPO_ROOT/seqs_amd/lib/diag/libframesum_$v.so" timeout -k 10 120 python tools/stamps.py --config $cfg > gpurun_out/stamps_${v}_$cfg.log 2>&1 || { echo "STAMPS FAILED"; tail -5 gpurun_out/stamps_${v}_$cfg.log; exit 1; }
