@@ -511,7 +511,7 @@ __device__ __forceinline__ void st8(uint8_t* p, uint32_t v) { *p = (uint8_t)v; }
 // verdict from the streamed sum `cs` and the parked parse, then the op's writes and stores.
 // `len` is the frame length the rows streamed (kOpsFcs: without the FCS).
 template <uint32_t kOps>
-__device__ __forceinline__ void finish_frame(const char* lds, uint32_t hw, uint32_t grp, uint64_t S, uint32_t len,
+__device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, uint64_t S, uint32_t len,
                                              uint32_t te, uint32_t Y, uint32_t cs, const uint8_t* frames,
                                              uint8_t* wframes, const uint32_t* lengths, uint32_t fi, uint2* out,
                                              uint8_t* status, uint32_t tx) {
@@ -520,7 +520,6 @@ __device__ __forceinline__ void finish_frame(const char* lds, uint32_t hw, uint3
         const uint8_t* fp = frames + S + len;
         fcs = (uint32_t)fp[0] | ((uint32_t)fp[1] << 8) | ((uint32_t)fp[2] << 16) | ((uint32_t)fp[3] << 24);
     }
-    const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
     const uint32_t sa = (uint32_t)S & 3u;
     const uint32_t* fbs = reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2));
     uint32_t crcv;
@@ -1186,6 +1185,8 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         // 4th -- still holds the up to 3 bytes past the frame end. Their CRC contribution is
         // that junk itself (the last dword enters the combine unshifted) and their sum is
         // sad16 of it: remove both.
+        // the parked parse, read by every lane now: its LDS round trip overlaps the combine's
+        const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
         uint32_t junk = 0u;
         if (T.P > 0 && T.H < T.P && gl == 3u && T.nd() > 0) junk = pf[kPrefetchA - 1].w & ~T.tail_mask();
         const uint32_t U =
@@ -1204,7 +1205,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         FS_STAMP(3);
         // ---- the group's lane 0: finish and store (its frame's parse comes back from LDS).
         if (parser)
-            finish_frame<kOps>(lds, hw, grp, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths,
+            finish_frame<kOps>(lds, P, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths,
                                tile * kFramesPerTile + grp, out, status, tx);
         FS_STAMP(4);
         FS_RTSTAMP(6);
@@ -1437,7 +1438,8 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
                     csum += sl.y;
                 }
             }
-            finish_frame<kOps>(lds, hw, grp, T.S, T.len, T.te(), Y, csum, frames, wframes, lengths,
+            finish_frame<kOps>(lds, unpark_parsed<kOps>(lds, hw, grp), T.S, T.len, T.te(), Y, csum, frames, wframes,
+                               lengths,
                                tile * kFramesPerTile + grp, out, status, tx);
         }
         FS_STAMP(4);
