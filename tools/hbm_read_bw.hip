@@ -33,12 +33,12 @@ __global__ void k_stream(const u32x4* __restrict__ p, size_t n16, uint32_t* out)
 }
 
 // G lanes per frame (64/G frames per wave), rows of G*16 bytes anchored at the frame end.
-template <int kPF, int G, bool NT = false>
-__global__ void __launch_bounds__(1024) k_frames(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
-                                                 uint32_t* out) {
+template <int kPF, int G, bool NT = false, int WPB = 16>
+__global__ void __launch_bounds__(64 * WPB) k_frames(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
+                                                     uint32_t* out) {
     constexpr int FPW = 64 / G, RD = 4 * G;  // frames per wave, row dwords
     const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
-    const uint32_t gwave = blockIdx.x * 16 + (threadIdx.x >> 6), nwaves = gridDim.x * 16;
+    const uint32_t gwave = blockIdx.x * WPB + (threadIdx.x >> 6), nwaves = gridDim.x * WPB;
     const uint32_t ntiles = (nframes + FPW - 1) / FPW;
     uint32_t acc = 0;
     for (uint32_t t = gwave; t < ntiles; t += nwaves) {
@@ -120,5 +120,13 @@ int main(int argc, char** argv) {
     FR(4, 16, true, cus, "frames G=16 PF=4 nt");
     FR(2, 64, false, cus, "frames G=64 PF=2");
     FR(2, 64, true, cus, "frames G=64 PF=2 nt");
+    // fewer waves per CU (one block of WPB waves per CU), deeper rings
+#define FRW(PF, WPB, NAME) timeit([&](int i) { hipLaunchKernelGGL((k_frames<PF, 4, false, WPB>), dim3(cus), dim3(64 * WPB), 0, 0, bufs[i % NB], nf, fl, out); }, NAME)
+    FRW(6, 16, "frames G=4  PF=6  16 waves/CU");
+    FRW(12, 8, "frames G=4  PF=12 8 waves/CU");
+    FRW(8, 8, "frames G=4  PF=8  8 waves/CU");
+    FRW(6, 8, "frames G=4  PF=6  8 waves/CU");
+    FRW(16, 4, "frames G=4  PF=16 4 waves/CU");
+    FRW(12, 12, "frames G=4  PF=12 12 waves/CU");
     return 0;
 }
