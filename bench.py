@@ -9,7 +9,10 @@ batches (> 256 MiB in total) are rotated so the 256 MiB Infinity Cache cannot
 serve them. Multi-GPU (torchrun, one process per GPU, RCCL = torch "nccl"):
 every rank digests its own shard (weak scaling, frame i of the global batch
 on rank i mod N) and the per-frame digests + verdicts are gathered to rank 0
-over RCCL, pipelined one step behind the kernels; no other collective.
+over RCCL, one gather per group of --gather-every steps, overlapped with the next
+group's kernels; no other collective. Rank 0 receives the shards as they are (global
+frame j*N + r is local frame j of rank r: seqs_amd.shard.gather_digests shows the
+interleave; the bench does not spend a rank-0 kernel on it).
 
 Prints ONE JSON line on rank 0 (see the contract in DESIGN.md §5).
 """
@@ -45,6 +48,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
     p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather (N>1 diagnostics)")
+    p.add_argument("--gather-every", type=int, default=64,
+                   help="N>1: each stream sends the digests + verdicts of this many of its steps to rank 0 in "
+                        "one RCCL gather (one collective per group, not two per step)")
+    p.add_argument("--force-gather", action="store_true",
+                   help="run the gather path on a single GPU too (a 1-rank process group; a test of the N>1 loop)")
     p.add_argument("--op", choices=["digest", "fill", "fcs"], default="digest",
                    help="digest: RX digest + verdict (the BASELINE metric); fill: TX checksum fill + FCS "
                         "append in place (fs_fill_batch); fcs: RX of wire frames carrying an FCS")
@@ -137,7 +145,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from seqs_amd import Engine, shard
+    from seqs_amd import Engine
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -146,6 +154,9 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+    elif args.force_gather and not args.no_gather:
+        dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1,
+                                init_method=f"tcp://127.0.0.1:{os.environ.get('MASTER_PORT', '29513')}")
 
     n = args.frames
     engine = Engine(local)
@@ -165,47 +176,70 @@ def main():
     resident = sum(int(x[0].numel()) for x in batches)
     nb = len(batches)
     ns = max(1, args.streams)
-    nslot = max(2, ns)
-    outs = [torch.empty((n, 2), dtype=torch.int32, device=dev) for _ in range(nslot)]
-    stats = [torch.empty((n,), dtype=torch.uint8, device=dev) for _ in range(nslot)]
-    gather = world > 1 and not args.no_gather
+    gather = dist.is_initialized() and not args.no_gather
     main_stream = torch.cuda.current_stream(dev)
     streams = [main_stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
-    # a slot's previous gather / kernel must be finished before the slot is rewritten
-    slot_done = [None] * nslot
+    # Output slots (digest words, then verdicts, in one 256-B-aligned slab per slot). Without a
+    # gather, step i writes slot i % nslot and slot k is only ever written by stream k (nslot ==
+    # ns for ns >= 2; one stream for ns == 1): stream order alone keeps a slot's launches apart.
+    # With the gather, each stream owns 2 groups of G slots for its own consecutive steps; when
+    # a group is full, that stream hands its slabs to rank 0 in one RCCL gather (issued on that
+    # stream, so it waits for that stream's kernels only) while it fills the other group.
+    G = max(1, args.gather_every) if gather else 1
+    nslot = max(2, ns)
+    slab = (9 * n + 255) // 256 * 256
 
-    pending = []
+    def views(buf, k):
+        base = k * slab
+        return buf[base : base + 8 * n].view(torch.int32).view(n, 2), buf[base + 8 * n : base + 9 * n]
+
+    if gather:
+        gbuf = [[torch.empty(G * slab, dtype=torch.uint8, device=dev) for _ in range(2)] for _ in range(ns)]
+        gviews = [[[views(gbuf[st][g], j) for j in range(G)] for g in range(2)] for st in range(ns)]
+        recv = [[[torch.empty_like(gbuf[st][g]) for _ in range(world)] if rank == 0 else None for g in range(2)]
+                for st in range(ns)]
+        pend = [[None, None] for _ in range(ns)]  # per stream and group: the RCCL work of its latest gather
+    flat = torch.empty(nslot * slab, dtype=torch.uint8, device=dev)
+    outs, stats = zip(*[views(flat, k) for k in range(nslot)])
 
     def step(i: int):
         fb, fo, fl = batches[i % nb]
-        k = i % nslot
-        s = streams[i % ns]
+        si = i % ns
+        s = streams[si]
         if not gather:
-            # slot k is only ever written by stream k (nslot == ns for ns >= 2; one stream for
-            # ns == 1): stream order alone keeps a slot's launches apart, no events needed
-            run_op(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=s)
+            run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=s)
             return
+        q = i // ns
+        g, j = (q // G) % 2, q % G
         with torch.cuda.stream(s):
-            if slot_done[k] is not None:
-                s.wait_event(slot_done[k])
-            run_op(fb, fo, fl, mtu=0, out=outs[k], status=stats[k], stream=s)
-            # digests of step i go to rank 0 over RCCL while later steps' kernels run;
-            # at most `nslot` gathers are pending (each slot is reused nslot steps later)
-            while len(pending) >= nslot:
-                pending.pop(0)()
-            _, finish = shard.gather_digests(outs[k], stats[k], world, rank, n * world, async_op=True)
-            pending.append(finish)
-            done = torch.cuda.Event()
-            done.record(s)
-            slot_done[k] = done
+            if j == 0 and pend[si][g] is not None:
+                pend[si][g].wait()  # this stream waits until the gather has read group g's slabs
+                pend[si][g] = None
+            o, st = gviews[si][g][j]
+            run_op(fb, fo, fl, mtu=0, out=o, status=st, stream=s)
+            if j == G - 1:
+                pend[si][g] = dist.gather(gbuf[si][g], recv[si][g], dst=0, async_op=True)
 
-    def drain():
-        while pending:
-            pending.pop(0)()
+    def drain(i_end: int):
+        if not gather:
+            return
+        # partly filled groups still go to rank 0 (same calls on every rank: i_end is common)
+        for si in range(ns):
+            q_end = (i_end - si + ns - 1) // ns  # steps this stream ran
+            g = (q_end // G) % 2
+            if q_end % G != 0 and pend[si][g] is None:
+                with torch.cuda.stream(streams[si]):
+                    pend[si][g] = dist.gather(gbuf[si][g], recv[si][g], dst=0, async_op=True)
+        for si in range(ns):
+            for g in range(2):
+                if pend[si][g] is not None:
+                    with torch.cuda.stream(streams[si]):
+                        pend[si][g].wait()
+                    pend[si][g] = None
 
     for i in range(args.warmup):
         step(i)
-    drain()
+    drain(args.warmup)
     torch.cuda.synchronize()
 
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks
@@ -215,7 +249,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
-    drain()
+    drain(args.warmup + args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -224,6 +258,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    if gather and rank == 0:
+        # every group's latest gather delivered rank 0's own slabs intact (a check of the loop)
+        torch.cuda.synchronize()
+        for si in range(ns):
+            for g in range(2):
+                assert torch.equal(recv[si][g][0], gbuf[si][g]), "gathered digests differ from rank 0's own"
 
     # ---- kernel-only timing with HIP events on the launch stream (roofline.achieved): one event
     # pair around K back-to-back launches on one stream (no overlap with another launch), so the
@@ -293,7 +334,7 @@ def main():
         }
         print(json.dumps(result), flush=True)
     engine.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return result
 
