@@ -1295,10 +1295,12 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     FS_STAMP(1);
 
     while (tile < ntiles) {
-        // Opaque copies of the lane indices: everything derived from them is recomputed per
-        // tile instead of being hoisted out of the tile loop into (spilled) registers.
-        uint32_t grp = grp0, gl = gl0;
-        asm volatile("" : "+v"(grp), "+v"(gl));
+        // The lane indices recomputed per tile from mbcnt (no register of the kernel's start
+        // stays live for them: they used to be spilled, and their reload at the loop head
+        // waited vmcnt(0), draining the tile's prefetched rows).
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        uint32_t grp = ln >> 2, gl = ln & 3u;
         const bool fvalid = tile * kFramesPerTile + grp < n;
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
         const int npass = T.npass;
