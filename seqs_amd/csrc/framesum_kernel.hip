@@ -92,17 +92,21 @@ constexpr int kHdrDwords = 32;
 constexpr int kHdrDmas = kHdrDwords / 4;
 constexpr uint32_t kHdrWaveBytes = 4u * kHdrDwords * kFramesPerTile;  // 2 KB
 
-// LDS map (bytes). [0, 100 KB) is the FsTables LDS image: region A built in place from
-// the Z64 basis, the plain tables copied by LDS-DMA.
-constexpr uint32_t kLdsZ32 = 65536;
+// LDS map (bytes). [0, 104 KB) holds the tables: the plain tables first (copied by LDS-DMA
+// from FsTables, where they follow region A), then region A (built in place from the Z64
+// basis). Every table address is a constant below 64 KB plus a lane-dependent part, so
+// hipcc folds the constant into the ds_read offset field instead of holding it in a VGPR.
+constexpr uint32_t kLdsZ32 = 0;
 constexpr uint32_t kLdsZ16 = kLdsZ32 + 4096;
 constexpr uint32_t kLdsZfin = kLdsZ16 + 4096;  // Z4, Z3, Z2, Z1 (4 KB each)
 constexpr uint32_t kLdsZ48 = kLdsZfin + 16384;
 constexpr uint32_t kLdsZ12 = kLdsZ48 + 4096;
 constexpr uint32_t kLdsZ8 = kLdsZ12 + 4096;
 constexpr uint32_t kLdsZ768 = kLdsZ8 + 4096;    // Z_768: shift past one full piece (mode B)
-constexpr uint32_t kLdsTables = kLdsZ768 + 4096;
+constexpr uint32_t kLdsRegionA = kLdsZ768 + 4096;  // 64 KB: [entry][table*8+copy], 256 B per entry
+constexpr uint32_t kLdsTables = kLdsRegionA + 65536;
 constexpr uint32_t kLdsHdr = kLdsTables;
+static_assert(kLdsRegionA < 65536, "ds_read offset field");
 // mode B pieces (see "Tiles, pieces and passes")
 constexpr int kPieceRows = 12;
 constexpr int kPieceDwords = kPieceRows * kRowDwords;  // 192 dwords = 768 bytes
@@ -114,8 +118,8 @@ constexpr uint32_t kLdsBytes = kLdsWave + kWavesPerBlock * kWaveScratchBytes;
 static_assert(kPieceRows % kPrefetch == 0, "a piece is whole blocks of rows");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kTablesLdsBytes == kLdsTables, "FsTables is the LDS image of the tables");
-constexpr uint32_t kPlainChunk0 = 65536 / 1024;                     // first 1-KB piece of the plain tables
-constexpr uint32_t kPlainChunks = (kLdsTables - 65536) / 1024;      // 40 pieces
+constexpr uint32_t kPlainChunk0 = 65536 / 1024;                     // first 1-KB piece of the plain tables in FsTables
+constexpr uint32_t kPlainChunks = kLdsRegionA / 1024;               // 40 pieces, to LDS [0, 40 KB)
 constexpr uint32_t kDmaPerWave = (kPlainChunks + kWavesPerBlock - 1) / kWavesPerBlock;
 
 // The workgroup's LDS image (static allocation of digest_kernel). Namespace scope, so the
@@ -186,10 +190,10 @@ __device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const Lane
         const uint32_t u2 = __builtin_amdgcn_perm(a, k.cvec, k.sel[2]), u3 = __builtin_amdgcn_perm(a, k.cvec, k.sel[3]);
         return xor3(xor3(u0, u1, u2), u3, w);
     }
-    uint32_t t0 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
-    uint32_t t1 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
-    uint32_t t2 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
-    uint32_t t3 = lds32(lds, __builtin_amdgcn_perm(a, k.cvec, k.sel[3]));
+    uint32_t t0 = lds32(lds, kLdsRegionA + __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
+    uint32_t t1 = lds32(lds, kLdsRegionA + __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
+    uint32_t t2 = lds32(lds, kLdsRegionA + __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
+    uint32_t t3 = lds32(lds, kLdsRegionA + __builtin_amdgcn_perm(a, k.cvec, k.sel[3]));
     return xor3(xor3(t0, t1, t2), t3, w);
 }
 
@@ -491,8 +495,8 @@ __device__ uint32_t finish_l4(const uint32_t* fb, uint32_t sa, uint32_t len, con
 __device__ __forceinline__ uint32_t zshift(const char* lds, uint32_t v, uint32_t k) {
     for (; k >= 768u; k -= 768u) v = zplain(lds, v, kLdsZ768);
     for (; k >= 64u; k -= 64u)
-        v = lds32(lds, (v & 0xffu) << 8) ^ lds32(lds, (((v >> 8) & 0xffu) << 8) + 32u) ^
-            lds32(lds, (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, ((v >> 24) << 8) + 96u);
+        v = lds32(lds, kLdsRegionA + ((v & 0xffu) << 8)) ^ lds32(lds, kLdsRegionA + (((v >> 8) & 0xffu) << 8) + 32u) ^
+            lds32(lds, kLdsRegionA + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kLdsRegionA + ((v >> 24) << 8) + 96u);
     if (k >= 48u) { v = zplain(lds, v, kLdsZ48); k -= 48u; }
     else if (k >= 32u) { v = zplain(lds, v, kLdsZ32); k -= 32u; }
     else if (k >= 16u) { v = zplain(lds, v, kLdsZ16); k -= 16u; }
@@ -891,7 +895,7 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
         const uint32_t m = 0u - ((e >> j) & 1u);
         v ^= basis[j] & m;
     }
-    u32x4* dst = reinterpret_cast<u32x4*>(lds + e * 256u + 32u * b);
+    u32x4* dst = reinterpret_cast<u32x4*>(lds + kLdsRegionA + e * 256u + 32u * b);
     dst[0] = u32x4{v, v, v, v};
     dst[1] = u32x4{v, v, v, v};
 }
@@ -929,8 +933,8 @@ __device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, con
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
     for (uint32_t k = 0; k < ((FS_DIAG & 2) ? 0 : kDmaPerWave); ++k) {
-        const uint32_t c = kPlainChunk0 + min(w0 + k * kWavesPerBlock, kPlainChunks - 1u);
-        dma_x4(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
+        const uint32_t c = min(w0 + k * kWavesPerBlock, kPlainChunks - 1u);
+        dma_x4(reinterpret_cast<const char*>(tabs) + (kPlainChunk0 + c) * 1024u + lane * 16u,
                __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
     }
 }
