@@ -229,3 +229,33 @@ def test_host_staged_rejects_out_of_range(engine):
     buf = np.zeros(100, np.uint8)
     with pytest.raises(Exception):
         engine.digest_host(buf, np.array([90], np.uint64), np.array([20], np.uint32))
+
+
+def test_random_batch_stress(engine):
+    # many independent random batches: sizes from 1 frame to several tiles per wave, lengths
+    # from 0 to jumbo (some batches uniform, some mixed), random gaps and start alignments,
+    # valid / corrupted / random frames, random MTU; every digest and verdict bit-exact
+    rng = np.random.default_rng(2024)
+    for it in range(24):
+        n = int(rng.choice([1, 7, 16, 300, 4096, 20000, 70000]))
+        kind = it % 3
+        if kind == 0:  # uniform length
+            ln = np.full(n, int(rng.choice([60, 64, 128, 577, 1500, 4000, 9000])), np.int64)
+        elif kind == 1:  # mixed
+            ln = rng.choice([0, 3, 34, 54, 64, 200, 576, 1500, 9000], size=n).astype(np.int64)
+        else:  # anything up to jumbo
+            ln = rng.integers(0, 9200, n).astype(np.int64)
+        gaps = rng.integers(0, 9, n) if it % 2 else np.zeros(n, np.int64)
+        off = np.zeros(n, np.int64)
+        off[1:] = np.cumsum(ln[:-1] + gaps[:-1])
+        off += int(rng.integers(0, 4))
+        buf = rng.integers(0, 256, int(off[-1] + ln[-1] + 16), dtype=np.uint8)
+        # about half the frames well-formed TCP/UDP (some then corrupted)
+        sel = np.nonzero((ln >= 54) & (rng.random(n) < 0.5))[0]
+        for i in sel[:3000]:
+            f = synth.make_frames(1, int(ln[i]), 6 if i % 2 else 17, rng)[0]
+            if rng.random() < 0.1:
+                f[int(rng.integers(14, len(f)))] ^= 0x40
+            buf[off[i] : off[i] + ln[i]] = f
+        mtu = int(rng.choice([0, 0, 1514, 9018]))
+        check(engine, buf, off, ln.astype(np.int32), mtu=mtu, label=f"stress{it}/n={n}/kind={kind}")
