@@ -97,6 +97,8 @@ fs_status fs_ctx_destroy(fs_ctx* ctx);
 /* Message for the last failing call on `ctx` (or of fs_ctx_create when ctx is NULL). */
 const char* fs_last_error(const fs_ctx* ctx);
 
+/* Every batched call takes at most 2^31 frames (n); larger n is FS_E_INVALID. */
+
 /* Batched digest, device-resident. All pointers are DEVICE pointers.
  *   frame i = frames[offsets[i] : offsets[i] + lengths[i]]  (any byte alignment,
  *   frames may overlap or be sparse; the engine may read up to 3 bytes past a

@@ -22,6 +22,8 @@ using framesum::FsTables;
 constexpr int kHostSlots = 3;
 constexpr uint64_t kChunkBytes = 16ull << 20;
 constexpr uint32_t kChunkFrames = 1u << 20;
+// Frames per call: tile and frame indices are 32-bit in the kernel (n + 15 must not wrap).
+constexpr uint32_t kMaxFrames = 1u << 31;
 
 struct HostSlot {
     hipEvent_t copied = nullptr, consumed = nullptr;
@@ -206,6 +208,7 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
                           uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status, void* stream) {
     if (!ctx) return FS_E_INVALID;
     if (n == 0) return FS_SUCCESS;
+    if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_digest_batch: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_digest_batch: null pointer");
     if (reinterpret_cast<uintptr_t>(frames) & 3u)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch: frames must be 4-byte aligned");
@@ -221,6 +224,7 @@ fs_status fs_fill_batch(fs_ctx* ctx, uint8_t* frames, const uint64_t* offsets, c
     if (!ctx) return FS_E_INVALID;
     if (flags & ~(uint32_t)(FS_FILL_CSUM | FS_FCS_APPEND)) return set_err(ctx, FS_E_INVALID, "fs_fill_batch: unknown flags");
     if (n == 0) return FS_SUCCESS;
+    if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_fill_batch: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_fill_batch: null pointer");
     if (reinterpret_cast<uintptr_t>(frames) & 3u)
         return set_err(ctx, FS_E_INVALID, "fs_fill_batch: frames must be 4-byte aligned");
@@ -235,6 +239,7 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
                               uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status, void* stream) {
     if (!ctx) return FS_E_INVALID;
     if (n == 0) return FS_SUCCESS;
+    if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_fcs: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_fcs: null pointer");
     if (reinterpret_cast<uintptr_t>(frames) & 3u)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_fcs: frames must be 4-byte aligned");
@@ -249,6 +254,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status) {
     if (!ctx) return FS_E_INVALID;
     if (n == 0) return FS_SUCCESS;
+    if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: null pointer");
     FS_HIP(ctx, hipSetDevice(ctx->device));
@@ -327,6 +333,7 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
     if (flags & ~(uint32_t)(FS_FILL_CSUM | FS_FCS_APPEND))
         return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: unknown flags");
     if (n == 0) return FS_SUCCESS;
+    if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: null pointer");
     // One staged span [lo, hi) (the frames and, with FS_FCS_APPEND, their FCS bytes), copied in,
     // filled, copied back. Not chunk-pipelined: written spans of unordered batches may interleave.

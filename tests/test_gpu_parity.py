@@ -259,3 +259,13 @@ def test_random_batch_stress(engine):
             buf[off[i] : off[i] + ln[i]] = f
         mtu = int(rng.choice([0, 0, 1514, 9018]))
         check(engine, buf, off, ln.astype(np.int32), mtu=mtu, label=f"stress{it}/n={n}/kind={kind}")
+
+
+def test_too_many_frames_rejected(engine):
+    import ctypes
+
+    dev = torch.device("cuda:0")
+    t = torch.zeros(64, dtype=torch.uint8, device=dev)
+    p = ctypes.c_void_p(t.data_ptr())
+    st = engine.lib.fs_digest_batch(engine._ctx, p, p, p, (1 << 31) + 1, 0, p, p, None)
+    assert st == -1 and b"too large" in engine.lib.fs_last_error(engine._ctx)
