@@ -629,10 +629,12 @@ struct Unit {
 
 __device__ __forceinline__ void tile_descriptors(uint32_t tile, uint32_t grp, uint32_t n,
                                                  const uint64_t* __restrict__ offsets,
-                                                 const uint32_t* __restrict__ lengths, uint64_t& S, uint32_t& len) {
-    const uint32_t fi = tile * kFramesPerTile + grp;
-    // groups past the batch end read the last frame's descriptor (their length is zeroed)
-    const uint32_t fl = fi < n ? fi : n - 1u;
+                                                 const uint32_t* __restrict__ lengths, uint64_t& S, uint32_t& len,
+                                                 uint32_t fpt = kFramesPerTile) {
+    const uint32_t fi = tile * fpt + grp;
+    // groups past the batch end (or past the tile's fpt frames) read the last frame's
+    // descriptor (their length is zeroed)
+    const uint32_t fl = (grp < fpt && fi < n) ? fi : n - 1u;
     // Inline asm: hipcc otherwise sinks the loads into their first use, serializing two HBM
     // round trips. The values are tied to an explicit wait (descriptors_ready) before use.
     asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(S) : "v"(offsets + fl));
@@ -711,8 +713,8 @@ __device__ __forceinline__ void pass0_unit(Unit& U, const Tile& T, int ndp, uint
 
 __device__ __forceinline__ void tile_geometry(Tile& T, Unit& U, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
                                               uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
-                                              char* lds, const WaveScratch& ws) {
-    T.len = (tile * kFramesPerTile + grp < n) ? len : 0u;
+                                              char* lds, const WaveScratch& ws, uint32_t fpt) {
+    T.len = (grp < fpt && tile * fpt + grp < n) ? len : 0u;
     T.S = S;
     const int nd = T.nd();
     const int rows = (nd + kRowDwords - 1) / kRowDwords;
@@ -821,8 +823,9 @@ struct TileA {
 };
 
 __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
-                                              uint64_t S, uint32_t len, const uint8_t* __restrict__ frames) {
-    T.len = (tile * kFramesPerTile + grp < n) ? len : 0u;
+                                              uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
+                                              uint32_t fpt) {
+    T.len = (grp < fpt && tile * fpt + grp < n) ? len : 0u;
     T.S = S;
     const int nd = T.nd();
     const int rows = (nd + kRowDwords - 1) / kRowDwords;
@@ -1025,7 +1028,7 @@ template <uint32_t kOps>
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
                 const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
-                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx) {
+                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx, uint32_t fpt) {
     char* lds = g_lds;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1034,7 +1037,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     const uint32_t gl = lane & 3u;    // lane within the group
     const uint32_t gwave = blockIdx.x * kWavesPerBlock + wave;
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-    const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
+    // fpt: frames per tile (16, or 8 / 4 for batches too small to give every wave a tile;
+    // the other groups stay empty)
+    fpt = __builtin_amdgcn_readfirstlane(fpt);
+    const uint32_t ntiles = (n + fpt - 1) / fpt;
     const uint32_t hw = kLdsHdr + wave * kHdrWaveBytes;  // this wave's header slots
 
     LaneKeys keys;
@@ -1064,14 +1070,14 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         uint64_t S;
         uint32_t len;
         if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(3);  // the preamble outranks other waves' row loops
-        tile_descriptors(tile, grp, n, offsets, lengths, S, len);
+        tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
         build_region_a(tabs, lds);
         FS_STAMP(7);
         descriptors_ready<kOps>(S, len);
         FS_STAMP(8);
         T.P = 0;
         if (first) {
-            tile_geometry_a(T, tile, grp, gl, n, S, len, frames);
+            tile_geometry_a(T, tile, grp, gl, n, S, len, frames, fpt);
             if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
         }
     }
@@ -1102,7 +1108,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
 
         uint32_t A[4] = {0u, 0u, 0u, 0u};
         uint32_t cs = 0u;
-        const bool fvalid = tile * kFramesPerTile + grp < n;
+        const bool fvalid = grp < fpt && tile * fpt + grp < n;
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
 
         // ---- header parse: after the first block of rows, while the ring's loads are in flight.
@@ -1210,16 +1216,16 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         // ---- the group's lane 0: finish and store (its frame's parse comes back from LDS).
         if (parser)
             finish_frame<kOps>(lds, P, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths,
-                               tile * kFramesPerTile + grp, out, status, tx);
+                               tile * fpt + grp, out, status, tx);
         FS_STAMP(4);
         FS_RTSTAMP(6);
         tile += nwaves;
         if (tile < ntiles) {  // next tile: descriptors, geometry, header DMA, row prefetch
             uint64_t S;
             uint32_t len;
-            tile_descriptors(tile, grp, n, offsets, lengths, S, len);
+            tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
             descriptors_ready<kOps>(S, len);
-            tile_geometry_a(T, tile, grp, gl, n, S, len, frames);
+            tile_geometry_a(T, tile, grp, gl, n, S, len, frames, fpt);
             if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             header_dma<true>(T, frames, lds, hw, gl, lane);
             if (T.P > 0) {
@@ -1238,7 +1244,8 @@ template <uint32_t kOps>
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
                  const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
-                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx) {
+                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx,
+                 uint32_t fpt) {
     char* lds = g_lds;
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1247,7 +1254,8 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     const uint32_t gl0 = lane & 3u;    // lane within the group
     const uint32_t gwave = blockIdx.x * kWavesPerBlock + wave;
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-    const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
+    fpt = __builtin_amdgcn_readfirstlane(fpt);  // frames per tile (16, 8 or 4; see launch_digest)
+    const uint32_t ntiles = (n + fpt - 1) / fpt;
     const uint32_t hw = kLdsHdr + wave * kHdrWaveBytes;  // this wave's header slots
     WaveScratch ws;
     ws.ftab = kLdsWave + wave * kWaveScratchBytes;
@@ -1282,11 +1290,11 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     {
         uint64_t S;
         uint32_t len;
-        tile_descriptors(tile, grp0, n, offsets, lengths, S, len);
+        tile_descriptors(tile, grp0, n, offsets, lengths, S, len, fpt);
         build_region_a(tabs, lds);
         descriptors_ready<kOps>(S, len);
         U.P = 0;
-        if (first) tile_geometry(T, U, tile, grp0, gl0, n, S, len, frames, lds, ws);
+        if (first) tile_geometry(T, U, tile, grp0, gl0, n, S, len, frames, lds, ws, fpt);
     }
     plain_dma(tabs, lds, wave, lane);
     bool x4 = false;
@@ -1305,7 +1313,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         uint32_t ln;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
         uint32_t grp = ln >> 2, gl = ln & 3u;
-        const bool fvalid = tile * kFramesPerTile + grp < n;
+        const bool fvalid = grp < fpt && tile * fpt + grp < n;
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
         const int npass = T.npass;
         const int total_rows = U.P + kPieceRows * (npass - 1);
@@ -1446,7 +1454,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             }
             finish_frame<kOps>(lds, unpark_parsed<kOps>(lds, hw, grp), T.S, T.len, T.te(), Y, csum, frames, wframes,
                                lengths,
-                               tile * kFramesPerTile + grp, out, status, tx);
+                               tile * fpt + grp, out, status, tx);
         }
         FS_STAMP(4);
         FS_RTSTAMP(6);
@@ -1454,9 +1462,9 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         if (tile < ntiles) {  // next tile: descriptors, geometry, header DMA, row prefetch
             uint64_t S;
             uint32_t len;
-            tile_descriptors(tile, grp, n, offsets, lengths, S, len);
+            tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
             descriptors_ready<kOps>(S, len);
-            tile_geometry(T, U, tile, grp, gl, n, S, len, frames, lds, ws);
+            tile_geometry(T, U, tile, grp, gl, n, S, len, frames, lds, ws, fpt);
             header_dma<false>(T, frames, lds, hw, gl, lane);
             prefetch_unit(U, pf);
         }
@@ -1476,10 +1484,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
                          int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force, FsOp op,
                          uint8_t* wframes, uint32_t tx) {
     if (n == 0) return hipSuccess;
-    const uint32_t ntiles = (n + kFramesPerTile - 1) / kFramesPerTile;
-    uint32_t blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t max_blocks = (uint32_t)(num_cus > 0 ? num_cus : 256);
-    if (blocks > max_blocks) blocks = max_blocks;
     // The report of the launches before (the latest launch id that met a mixed-length tile):
     // launches are enqueued ahead of the GPU, so a report arrives several launches late; the
     // mixed kernel stays chosen for kStickyLaunches launches after the latest report (it keeps
@@ -1498,10 +1503,19 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         mixed = latest != 0u && ((id - latest) & 0xFFFFu) <= kStickyLaunches;
     }
     if (force) mixed = force == 2;
+    // Fewer frames per tile (8, then 4) while 16 would leave waves without a tile: a small
+    // batch still spreads over every CU. The groups past a tile's frames stay empty in the
+    // one-pass kernel; the mixed-length kernel gives them pieces of the tile's long frames.
+    uint32_t fpt = kFramesPerTile;
+    const uint32_t waves = max_blocks * (uint32_t)kWavesPerBlock;
+    while (fpt > 4u && (n + fpt - 1) / fpt < waves) fpt >>= 1;
+    const uint32_t tiles = (n + fpt - 1) / fpt;
+    uint32_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (blocks > max_blocks) blocks = max_blocks;
     uint2* o = reinterpret_cast<uint2*>(out);
 #define FS_LAUNCH(K, OPS)                                                                                   \
     hipLaunchKernelGGL((K<OPS>), dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
-                       tables, o, status, report, wframes, tx)
+                       tables, o, status, report, wframes, tx, fpt)
     switch (op) {
     case FsOp::kDigest:
         if (mixed) FS_LAUNCH(digest_kernel_ab, kOpsDigest);

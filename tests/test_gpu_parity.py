@@ -269,3 +269,12 @@ def test_too_many_frames_rejected(engine):
     p = ctypes.c_void_p(t.data_ptr())
     st = engine.lib.fs_digest_batch(engine._ctx, p, p, p, (1 << 31) + 1, 0, p, p, None)
     assert st == -1 and b"too large" in engine.lib.fs_last_error(engine._ctx)
+
+
+@pytest.mark.parametrize("n,flen", [(40000, 1500), (16384, 9000), (2000, 9000), (3000, 64)])
+def test_frames_per_tile_adaptation(engine, n, flen):
+    # batches too small to give every wave a 16-frame tile run the one-pass kernel with 8 or
+    # 4 frames per tile (40,000 frames: 8; 16,384 jumbo frames: 4), the empty groups idle
+    buf, off, ln = synth.uniform_batch(n, flen, seed=n)
+    crc, ipc, l4c, st = check(engine, buf, off, ln, label=f"fpt n={n} len={flen}")
+    assert (st == 0).all()
