@@ -278,3 +278,19 @@ def test_frames_per_tile_adaptation(engine, n, flen):
     buf, off, ln = synth.uniform_batch(n, flen, seed=n)
     crc, ipc, l4c, st = check(engine, buf, off, ln, label=f"fpt n={n} len={flen}")
     assert (st == 0).all()
+
+
+@pytest.mark.parametrize("n,flen", [(300000, 0), (1 << 20, 64), (200000, 1500)])
+def test_many_tiles_per_wave(engine, n, flen):
+    # several tiles per wave: the one-pass kernel's tile loop carries its descriptor, header
+    # and row prefetch across tiles (flen 0: random lengths up to 2 KB)
+    if flen:
+        buf, off, ln = synth.uniform_batch(n, flen, seed=n)
+    else:
+        rng = np.random.default_rng(n)
+        ln = rng.integers(0, 2048, n).astype(np.int64)
+        off = np.zeros(n, np.int64)
+        off[1:] = np.cumsum(ln[:-1] + 3)
+        buf = rng.integers(0, 256, int(off[-1] + ln[-1] + 16), dtype=np.uint8)
+        ln = ln.astype(np.int32)
+    check(engine, buf, off, ln, label=f"many tiles n={n} len={flen}")
