@@ -2,6 +2,7 @@
 //  k_stream : grid-stride global_load_dwordx4, 16 B/lane, fully coalesced (chip ceiling)
 //  k_frames : the digest kernel's pattern without compute — 16 frames per wave,
 //             4 lanes per frame, 64-B end-anchored rows, kPF rows in flight
+//  k_frames_al : the same with rows aligned to 64 or 128 B in memory
 // Both rotate NB distinct 98.3 MB buffers (> 256 MiB Infinity Cache).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -69,6 +70,42 @@ __global__ void __launch_bounds__(64 * WPB) k_frames(const uint8_t* __restrict__
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// Same as k_frames but rows are 64-B aligned in memory (no row straddles a 128-B line):
+// a frame covers blocks [S>>6, (E-1)>>6]; the partial head/tail blocks would be masked.
+template <int kPF, int WPB = 16, int RB = 64>
+__global__ void __launch_bounds__(64 * WPB) k_frames_al(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
+                                                        uint32_t* out) {
+    constexpr int G = RB / 16, FPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
+    const uint32_t gwave = blockIdx.x * WPB + (threadIdx.x >> 6), nwaves = gridDim.x * WPB;
+    const uint32_t ntiles = (nframes + FPW - 1) / FPW;
+    uint32_t acc = 0;
+    for (uint32_t t = gwave; t < ntiles; t += nwaves) {
+        uint32_t f = t * FPW + grp;
+        if (f >= nframes) f = nframes - 1;
+        const uint64_t S = (uint64_t)f * flen, E = S + flen;
+        const uint64_t b0 = S / RB, b1 = (E - 1) / RB;
+        const int R = (int)(b1 - b0 + 1);
+        const int Rp = (R + kPF - 1) / kPF * kPF;
+        // row r (0..Rp-1) reads block b1 - (Rp-1-r), clamped to b0
+        const u32x4* bl = reinterpret_cast<const u32x4*>(base) + b1 * (RB / 16) + gl;
+        const int first = -(Rp - 1);  // relative block of row 0
+        const int lo = -(R - 1);
+        u32x4 pf[kPF];
+#pragma unroll
+        for (int i = 0; i < kPF; ++i) pf[i] = bl[(RB / 16) * max(first + i, lo)];
+        for (int r0 = 0; r0 < Rp; r0 += kPF) {
+#pragma unroll
+            for (int i = 0; i < kPF; ++i) {
+                const int rel = first + r0 + i;
+                acc = (acc * 3) ^ pf[i].x ^ pf[i].y ^ pf[i].z ^ pf[i].w;
+                pf[i] = bl[(RB / 16) * max(min(rel + kPF, 0), lo)];
+            }
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const size_t nbytes = argc > 1 ? (size_t)atoll(argv[1]) : 98304000;
     const int NB = (int)((1200000000ull + nbytes - 1) / nbytes) < 4 ? 4 : (int)((1200000000ull + nbytes - 1) / nbytes);
@@ -128,5 +165,14 @@ int main(int argc, char** argv) {
     FRW(6, 8, "frames G=4  PF=6  8 waves/CU");
     FRW(16, 4, "frames G=4  PF=16 4 waves/CU");
     FRW(12, 12, "frames G=4  PF=12 12 waves/CU");
+#define FRA(PF, WPB, RB, NAME) timeit([&](int i) { hipLaunchKernelGGL((k_frames_al<PF, WPB, RB>), dim3(cus), dim3(64 * WPB), 0, 0, bufs[i % NB], nf, fl, out); }, NAME)
+    FRA(6, 16, 64, "aligned64 G=4 PF=6 16 waves/CU");
+    FRA(8, 16, 64, "aligned64 G=4 PF=8 16 waves/CU");
+    FRA(4, 16, 64, "aligned64 G=4 PF=4 16 waves/CU");
+    FRA(12, 8, 64, "aligned64 G=4 PF=12 8 waves/CU");
+    FRA(4, 16, 128, "aligned128 G=8 PF=4 16 waves/CU");
+    FRA(3, 16, 128, "aligned128 G=8 PF=3 16 waves/CU");
+    FRA(6, 8, 128, "aligned128 G=8 PF=6 8 waves/CU");
+    FRW(6, 16, "frames G=4  PF=6  16 waves/CU (again)");
     return 0;
 }
