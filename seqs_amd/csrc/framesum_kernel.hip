@@ -69,6 +69,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_PRE_PRIO
 #define FS_PRE_PRIO 0  // s_setprio(3) through the preamble (one-pass kernel)
 #endif
+#ifndef FS_TILE_MAP
+#define FS_TILE_MAP 1  // first tile of a wave: 0 block-major, 1 wave-major, 2 a contiguous 1/8 per XCD
+#endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio per block of rows
 #endif
@@ -1024,6 +1027,16 @@ __device__ __forceinline__ void post_report(uint64_t report) {
 // The kernel for batches of similar lengths: every tile in mode A (one pass). It reports in
 // `report` whether any tile would have run better in mode B, so that the host launches
 // digest_kernel_ab next time (launch_digest).
+// The wave's first tile (later tiles: + all waves). Every map is a bijection on [0, nwaves).
+__device__ __forceinline__ uint32_t first_tile(uint32_t wave) {
+    if (FS_TILE_MAP == 1) return wave * gridDim.x + blockIdx.x;
+    if (FS_TILE_MAP == 2 && (gridDim.x & 7u) == 0u) {  // workgroup b runs on XCD b % 8
+        const uint32_t per = gridDim.x >> 3;
+        return ((blockIdx.x & 7u) * per + (blockIdx.x >> 3)) * kWavesPerBlock + wave;
+    }
+    return blockIdx.x * kWavesPerBlock + wave;
+}
+
 template <uint32_t kOps>
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
@@ -1035,7 +1048,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t grp = lane >> 2;   // frame slot of this lane's group
     const uint32_t gl = lane & 3u;    // lane within the group
-    const uint32_t gwave = blockIdx.x * kWavesPerBlock + wave;
+    const uint32_t gwave = first_tile(wave);
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
     // fpt: frames per tile (16, or 8 / 4 for batches too small to give every wave a tile;
     // the other groups stay empty)
@@ -1252,7 +1265,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR addresses
     const uint32_t grp0 = lane >> 2;   // frame slot of this lane's group
     const uint32_t gl0 = lane & 3u;    // lane within the group
-    const uint32_t gwave = blockIdx.x * kWavesPerBlock + wave;
+    const uint32_t gwave = first_tile(wave);
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
     fpt = __builtin_amdgcn_readfirstlane(fpt);  // frames per tile (16, 8 or 4; see launch_digest)
     const uint32_t ntiles = (n + fpt - 1) / fpt;
