@@ -153,6 +153,21 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status);
 
+/* Multi-GPU form of fs_digest_batch_host for one host process (BASELINE configs[4]: frames
+ * streamed from host memory to several GPUs; SURVEY.md §8b fs_digest_batch_multi). Replaces
+ * the same per-frame calls as fs_digest_batch_host (stacks/portstack.go:163 RecvEth ->
+ * :240 / :303 CalculateChecksumIPv4), for a NIC ring too large for one GPU's PCIe link.
+ * The batch is cut into nctx contiguous blocks of frames holding about equal byte counts;
+ * block k runs on ctxs[k] (one context per GPU; several contexts may share a GPU), every
+ * block at once, each on its own host thread with its own H2D / kernel / D2H pipeline.
+ * A block's digests and verdicts are copied straight into out/status at the block's own
+ * indices: the host arrays are the gather, so no device collective is involved.
+ * ctxs must be distinct. Returns when every block is done; on failure, the status of the
+ * lowest failing block, whose message is in fs_last_error of that block's context. */
+fs_status fs_digest_batch_multi(fs_ctx* const* ctxs, int nctx, const uint8_t* frames, uint64_t frames_bytes,
+                                const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint32_t mtu,
+                                fs_digest* out, uint8_t* status);
+
 /* Kernel variant of a context's launches. The engine has two: a one-pass kernel
  * for batches of similar frame lengths, and one that splits long frames into
  * 768-byte pieces when a tile of 16 frames mixes very different lengths. By

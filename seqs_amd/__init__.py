@@ -14,6 +14,7 @@ from .framesum import (  # noqa: F401
     Digest,
     Engine,
     FramesumError,
+    digest_host_multi,
     lib_path,
     load_library,
     pack_frames,
@@ -30,6 +31,7 @@ __all__ = [
     "Digest",
     "Engine",
     "FramesumError",
+    "digest_host_multi",
     "lib_path",
     "load_library",
     "pack_frames",

@@ -7,6 +7,8 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/framesum.h"
 #include "framesum_internal.h"
@@ -379,6 +381,52 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
     FS_HIP(ctx, hipStreamSynchronize(ks));
     std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
     if (status) std::memcpy(status, h_st, n);
+    return FS_SUCCESS;
+}
+
+fs_status fs_digest_batch_multi(fs_ctx* const* ctxs, int nctx, const uint8_t* frames, uint64_t frames_bytes,
+                                const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint32_t mtu,
+                                fs_digest* out, uint8_t* status) {
+    if (!ctxs || nctx <= 0) return FS_E_INVALID;
+    for (int k = 0; k < nctx; ++k) {
+        if (!ctxs[k]) return FS_E_INVALID;
+        for (int j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k])
+                return set_err(ctxs[k], FS_E_INVALID, "fs_digest_batch_multi: a context appears twice in ctxs");
+    }
+    if (n == 0) return FS_SUCCESS;
+    if (n > kMaxFrames)
+        return set_err(ctxs[0], FS_E_INVALID, "fs_digest_batch_multi: n too large (at most 2^31 frames per call)");
+    if (!frames || !offsets || !lengths || !out)
+        return set_err(ctxs[0], FS_E_INVALID, "fs_digest_batch_multi: null pointer");
+    // block k = frames [cut[k], cut[k+1]): the first frame whose running byte count reaches
+    // k/nctx of the total starts block k (contiguous blocks: one H2D stream per GPU)
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += lengths[i];
+    std::vector<uint32_t> cut(nctx + 1, n);
+    cut[0] = 0;
+    {
+        uint64_t run = 0;
+        int k = 1;
+        for (uint32_t i = 0; i < n && k < nctx; ++i) {
+            while (k < nctx && (unsigned __int128)run * nctx >= (unsigned __int128)total * k) cut[k++] = i;
+            run += lengths[i];
+        }
+    }
+    std::vector<fs_status> st(nctx, FS_SUCCESS);
+    auto run_block = [&](int k) {
+        const uint32_t b0 = cut[k], b1 = cut[k + 1];
+        if (b1 > b0)
+            st[k] = fs_digest_batch_host(ctxs[k], frames, frames_bytes, offsets + b0, lengths + b0, b1 - b0, mtu,
+                                         out + b0, status ? status + b0 : nullptr);
+    };
+    std::vector<std::thread> workers;
+    workers.reserve(nctx - 1);
+    for (int k = 1; k < nctx; ++k) workers.emplace_back(run_block, k);
+    run_block(0);
+    for (auto& w : workers) w.join();
+    for (int k = 0; k < nctx; ++k)
+        if (st[k] != FS_SUCCESS) return st[k];
     return FS_SUCCESS;
 }
 

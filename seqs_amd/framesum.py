@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = (
     "fs_fill_batch",
     "fs_fill_batch_host",
     "fs_digest_batch_fcs",
+    "fs_digest_batch_multi",
     "fs_ctx_set_kernel",
     "fs_host_alloc",
     "fs_host_free",
@@ -115,6 +116,8 @@ def load_library() -> ctypes.CDLL:
     lib.fs_digest_batch_fcs.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp]
     lib.fs_digest_batch_fcs.restype = ctypes.c_int32
     lib.fs_ctx_set_kernel.argtypes = [vp, ctypes.c_int]
+    lib.fs_digest_batch_multi.restype = i32
+    lib.fs_digest_batch_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, u64, vp, vp, u32, u32, vp, vp]
     lib.fs_host_alloc.restype = i32
     lib.fs_host_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
     lib.fs_host_free.restype = i32
@@ -347,6 +350,32 @@ class Engine:
         self.fill_host(buf, offsets, lengths, mtu, FILL_CSUM | (FCS_APPEND if append_fcs else 0))
         return [bytes(buf[int(o) : int(o) + int(l) + room]) for o, l in zip(offsets, lengths)]
 
+
+
+def digest_host_multi(engines: Sequence["Engine"], frames: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
+                      mtu: int = 0):
+    """Host buffers in, host results out, over several contexts at once (fs_digest_batch_multi):
+    contiguous byte-balanced blocks of frames, one per engine (one per GPU), each on its own
+    host thread and H2D / kernel / D2H pipeline. Returns (digests, status) in batch order."""
+    assert len(engines) > 0 and len({id(e) for e in engines}) == len(engines), "engines must be distinct"
+    lib = engines[0].lib
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = int(lengths.size)
+    assert offsets.size == n
+    out = np.zeros(n, dtype=DIGEST_DTYPE)
+    status = np.zeros(n, dtype=np.uint8)
+    if n == 0:
+        return out, status
+    ctxs = (ctypes.c_void_p * len(engines))(*[e._ctx for e in engines])
+    st = lib.fs_digest_batch_multi(ctxs, len(engines), frames.ctypes.data_as(ctypes.c_void_p), frames.nbytes,
+                                   offsets.ctypes.data_as(ctypes.c_void_p), lengths.ctypes.data_as(ctypes.c_void_p),
+                                   n, mtu, out.ctypes.data_as(ctypes.c_void_p), status.ctypes.data_as(ctypes.c_void_p))
+    if st != FS_SUCCESS:
+        msgs = "; ".join(f"ctx {k}: {e.lib.fs_last_error(e._ctx).decode()}" for k, e in enumerate(engines))
+        raise FramesumError(f"fs_digest_batch_multi failed ({st}): {msgs}")
+    return out, status
 
 def pack_frames(frames: Sequence[bytes], align: int = 4):
     """Pack a list of frames into one buffer (each frame at an `align`-aligned offset)."""

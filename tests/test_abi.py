@@ -71,3 +71,15 @@ def test_product_does_not_reference_oracle():
                 assert not pat.search(open(os.path.join(dirpath, fn)).read()), fn
     out = __import__("subprocess").run(["nm", "-D", seqs_amd.lib_path()], capture_output=True, text=True).stdout
     assert "oracle_" not in out
+
+
+def test_multi_rejects_bad_context_lists():
+    # argument checks of fs_digest_batch_multi run before any device call
+    import ctypes
+
+    lib = framesum.load_library()
+    none = ctypes.c_void_p()
+    assert lib.fs_digest_batch_multi(None, 1, none, 0, none, none, 1, 0, none, none) == -1
+    ctxs = (ctypes.c_void_p * 2)(None, None)
+    assert lib.fs_digest_batch_multi(ctxs, 0, none, 0, none, none, 1, 0, none, none) == -1
+    assert lib.fs_digest_batch_multi(ctxs, 2, none, 0, none, none, 1, 0, none, none) == -1

@@ -225,6 +225,37 @@ def test_piece_boundaries_and_mixed_tiles(engine):
         check(engine, buf, off, ln, mtu=1514, label=f"pieces/align{align}/mtu")
 
 
+def test_host_multi_contexts(engine):
+    # fs_digest_batch_multi: byte-balanced contiguous blocks over 1, 2, 3 and 5 contexts (all on
+    # this one GPU here; one per GPU in production), mixed lengths in shuffled buffer order,
+    # more contexts than frames, MTU gates; digests and verdicts land in batch order
+    from seqs_amd import Engine, digest_host_multi
+
+    extra = [Engine(0) for _ in range(4)]
+    try:
+        buf, off0, ln0 = synth.mixed_batch(9000, seed=21)
+        perm = np.random.default_rng(5).permutation(len(ln0))
+        for order in (np.arange(len(ln0)), perm):
+            off, ln = off0[order].astype(np.uint64), ln0[order].astype(np.uint32)
+            for mtu in (0, 1514):
+                edig, est = coracle.digest_batch(buf, off.astype(np.int64), ln.astype(np.int32), mtu)
+                for k in (1, 2, 3, 5):
+                    dig, st = digest_host_multi([engine] + extra[: k - 1], buf, off, ln, mtu)
+                    assert np.array_equal(dig, edig) and np.array_equal(st, est), (k, mtu)
+        few_off, few_ln = off0[:3].astype(np.uint64), ln0[:3].astype(np.uint32)
+        edig, est = coracle.digest_batch(buf, few_off.astype(np.int64), few_ln.astype(np.int32))
+        dig, st = digest_host_multi([engine] + extra, buf, few_off, few_ln)
+        assert np.array_equal(dig, edig) and np.array_equal(st, est)
+        dig, st = digest_host_multi([engine] + extra, buf, np.zeros(0, np.uint64), np.zeros(0, np.uint32))
+        assert dig.size == 0
+        with pytest.raises(Exception):  # a frame past the buffer fails its block's call
+            digest_host_multi([engine, extra[0]], np.zeros(100, np.uint8), np.array([0, 90], np.uint64),
+                              np.array([20, 20], np.uint32))
+    finally:
+        for e in extra:
+            e.close()
+
+
 def test_host_staged_rejects_out_of_range(engine):
     buf = np.zeros(100, np.uint8)
     with pytest.raises(Exception):

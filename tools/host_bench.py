@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from seqs_amd import Engine, synth  # noqa: E402
+from seqs_amd import Engine, digest_host_multi, synth  # noqa: E402
 
 
 def rate(fn, nbytes, reps):
@@ -50,6 +50,21 @@ def main():
             assert int(st.max()) == 0, "synthetic frames must verify"
             print(json.dumps({"case": f"{name}, host-staged ({kind})", "GiB_s": round(g, 2), "ms_per_batch": round(ms, 3),
                               "bytes": nbytes}), flush=True)
+    # fs_digest_batch_multi: one context per visible GPU (C5's 8-GPU streaming form), and on a
+    # one-GPU box 2 contexts sharing it (the threading and block split; one PCIe link either way)
+    ndev = torch.cuda.device_count()
+    buf, off, ln = cases[1][1]
+    nbytes = int(ln.astype(np.int64).sum())
+    pin = eng.host_empty(buf.shape)
+    pin[:] = buf
+    layouts = [[0] * 2] if ndev == 1 else [list(range(ndev))]
+    for devs in layouts:
+        engs = [eng] + [Engine(d) for d in devs[1:]]
+        g, ms = rate(lambda: digest_host_multi(engs, pin, off.astype(np.uint64), ln.astype(np.uint32)), nbytes, 20)
+        print(json.dumps({"case": f"{cases[1][0]}, fs_digest_batch_multi over devices {devs} (pinned)",
+                          "GiB_s": round(g, 2), "ms_per_batch": round(ms, 3), "bytes": nbytes}), flush=True)
+        for e in engs[1:]:
+            e.close()
     eng.close()
 
 
