@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <chrono>
+#include <string>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -106,6 +108,48 @@ __global__ void __launch_bounds__(64 * WPB) k_frames_al(const uint8_t* __restric
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// The frames pattern behind a descriptor load (offsets read from memory, as the digest
+// kernel's first dependent round trip), with LDS reserved per workgroup so that 1 or 2
+// workgroups fit a CU: for back-to-back launches on several streams, does a second
+// resident workgroup hide one launch's start and tail behind another's rows?
+template <int kPF, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_frames_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                                                          uint32_t nframes, uint32_t flen, uint32_t* out) {
+    extern __shared__ uint32_t lds_res[];
+    constexpr int G = 4, FPW = 16, RD = 16;
+    const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
+    const uint32_t gwave = blockIdx.x * WPB + (threadIdx.x >> 6), nwaves = gridDim.x * WPB;
+    const uint32_t ntiles = (nframes + FPW - 1) / FPW;
+    uint32_t acc = 0;
+    lds_res[threadIdx.x] = threadIdx.x;
+    for (uint32_t t = gwave; t < ntiles; t += nwaves) {
+        uint32_t f = t * FPW + grp;
+        if (f >= nframes) f = nframes - 1;
+        const uint64_t S = offs[f], E = S + flen;
+        const uint64_t sdw = S >> 2;
+        const int nd = (int)(((E + 3) >> 2) - sdw);
+        const int R = (nd + RD - 1) / RD;
+        const int Rp = (R + kPF - 1) / kPF * kPF;
+        const int rel0 = nd - RD * Rp + 4 * (int)gl;
+        const int rel_last = rel0 + RD * (Rp - 1);
+        const uint32_t* fb = reinterpret_cast<const uint32_t*>(base + sdw * 4);
+        const int lo = -(int)min(sdw, (uint64_t)(1 << 24));
+        u32x4 pf[kPF];
+#pragma unroll
+        for (int i = 0; i < kPF; ++i) pf[i] = *reinterpret_cast<const u32x4_a4*>(fb + max(rel0 + RD * i, lo));
+        for (int r0 = 0; r0 < Rp; r0 += kPF) {
+#pragma unroll
+            for (int i = 0; i < kPF; ++i) {
+                const int rel = rel0 + RD * (r0 + i);
+                acc = (acc * 3) ^ pf[i].x ^ pf[i].y ^ pf[i].z ^ pf[i].w;
+                pf[i] = *reinterpret_cast<const u32x4_a4*>(fb + max(min(rel + RD * kPF, rel_last), lo));
+            }
+        }
+    }
+    __syncthreads();
+    if (acc == 0x12345678u) out[0] = acc + lds_res[(threadIdx.x + 1) % (64 * WPB)];
+}
+
 int main(int argc, char** argv) {
     const size_t nbytes = argc > 1 ? (size_t)atoll(argv[1]) : 98304000;
     const int NB = (int)((1200000000ull + nbytes - 1) / nbytes) < 4 ? 4 : (int)((1200000000ull + nbytes - 1) / nbytes);
@@ -124,6 +168,42 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
     printf("buffer %zu bytes, %d rotated\n", nbytes, NB);
+    if (argc > 2 && std::string(argv[2]) == "streams") {
+        // back-to-back launches of the descriptor-led pattern on 4 streams
+        const uint32_t fl = 1500, nf = (uint32_t)(nbytes / fl);
+        std::vector<uint64_t> h(nf);
+        for (uint32_t i = 0; i < nf; ++i) h[i] = (uint64_t)i * fl;
+        uint64_t* d_offs;
+        CHECK(hipMalloc(&d_offs, nf * 8ull));
+        CHECK(hipMemcpy(d_offs, h.data(), nf * 8ull, hipMemcpyHostToDevice));
+        hipStream_t st[4];
+        for (auto& x : st) CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        auto run = [&](auto kern, int wpb, int grid, size_t lds, int nstreams, const char* name) {
+            CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            const int reps = 400;
+            for (int pass = 0; pass < 2; ++pass) {
+                CHECK(hipDeviceSynchronize());
+                auto t0 = std::chrono::steady_clock::now();
+                for (int i = 0; i < reps; ++i)
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * wpb), lds, st[i % nstreams], bufs[i % NB], d_offs, nf, fl, out);
+                CHECK(hipDeviceSynchronize());
+                const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+                if (pass) printf("%-52s %9.2f us/step  %8.1f GB/s whole job\n", name, us, nbytes / (us * 1e-6) / 1e9);
+            }
+        };
+        for (int ns : {1, 4}) {
+            char nm[160];
+            snprintf(nm, sizeof nm, "desc 16 waves/WG, 150 KB LDS (1 WG/CU), %d stream(s)", ns);
+            run(k_frames_desc<6, 16>, 16, cus, 150 * 1024, ns, nm);
+            snprintf(nm, sizeof nm, "desc  8 waves/WG,  76 KB LDS (2 WG/CU), %d stream(s)", ns);
+            run(k_frames_desc<6, 8>, 8, 2 * cus, 76 * 1024, ns, nm);
+            snprintf(nm, sizeof nm, "desc  8 waves/WG, 150 KB LDS (1 WG/CU), %d stream(s)", ns);
+            run(k_frames_desc<6, 8>, 8, 2 * cus, 150 * 1024, ns, nm);
+            snprintf(nm, sizeof nm, "desc  4 waves/WG,  38 KB LDS (4 WG/CU), %d stream(s)", ns);
+            run(k_frames_desc<6, 4>, 4, 4 * cus, 38 * 1024, ns, nm);
+        }
+        return 0;
+    }
     auto timeit = [&](auto launch, const char* name) {
         for (int i = 0; i < 10; ++i) launch(i);
         CHECK(hipDeviceSynchronize());
