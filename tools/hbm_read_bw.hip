@@ -150,6 +150,42 @@ __global__ void __launch_bounds__(64 * WPB) k_frames_desc(const uint8_t* __restr
     if (acc == 0x12345678u) out[0] = acc + lds_res[(threadIdx.x + 1) % (64 * WPB)];
 }
 
+// k_frames_al's aligned rows behind the same descriptor load, for the multi-stream runs.
+template <int kPF, int WPB, int RB>
+__global__ void __launch_bounds__(64 * WPB) k_frames_desc_al(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                                                             uint32_t nframes, uint32_t flen, uint32_t* out) {
+    extern __shared__ uint32_t lds_res[];
+    constexpr int G = RB / 16, FPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63, grp = lane / G, gl = lane % G;
+    const uint32_t gwave = blockIdx.x * WPB + (threadIdx.x >> 6), nwaves = gridDim.x * WPB;
+    const uint32_t ntiles = (nframes + FPW - 1) / FPW;
+    uint32_t acc = 0;
+    lds_res[threadIdx.x] = threadIdx.x;
+    for (uint32_t t = gwave; t < ntiles; t += nwaves) {
+        uint32_t f = t * FPW + grp;
+        if (f >= nframes) f = nframes - 1;
+        const uint64_t S = offs[f], E = S + flen;
+        const uint64_t b0 = S / RB, b1 = (E - 1) / RB;
+        const int R = (int)(b1 - b0 + 1);
+        const int Rp = (R + kPF - 1) / kPF * kPF;
+        const u32x4* bl = reinterpret_cast<const u32x4*>(base) + b1 * (RB / 16) + gl;
+        const int first = -(Rp - 1), lo = -(R - 1);
+        u32x4 pf[kPF];
+#pragma unroll
+        for (int i = 0; i < kPF; ++i) pf[i] = bl[(RB / 16) * max(first + i, lo)];
+        for (int r0 = 0; r0 < Rp; r0 += kPF) {
+#pragma unroll
+            for (int i = 0; i < kPF; ++i) {
+                const int rel = first + r0 + i;
+                acc = (acc * 3) ^ pf[i].x ^ pf[i].y ^ pf[i].z ^ pf[i].w;
+                pf[i] = bl[(RB / 16) * max(min(rel + kPF, 0), lo)];
+            }
+        }
+    }
+    __syncthreads();
+    if (acc == 0x12345678u) out[0] = acc + lds_res[(threadIdx.x + 1) % (64 * WPB)];
+}
+
 int main(int argc, char** argv) {
     const size_t nbytes = argc > 1 ? (size_t)atoll(argv[1]) : 98304000;
     const int NB = (int)((1200000000ull + nbytes - 1) / nbytes) < 4 ? 4 : (int)((1200000000ull + nbytes - 1) / nbytes);
@@ -201,6 +237,22 @@ int main(int argc, char** argv) {
             run(k_frames_desc<6, 8>, 8, 2 * cus, 150 * 1024, ns, nm);
             snprintf(nm, sizeof nm, "desc  4 waves/WG,  38 KB LDS (4 WG/CU), %d stream(s)", ns);
             run(k_frames_desc<6, 4>, 4, 4 * cus, 38 * 1024, ns, nm);
+            snprintf(nm, sizeof nm, "desc aligned64 16 waves/WG, 150 KB LDS, %d stream(s)", ns);
+            run(k_frames_desc_al<6, 16, 64>, 16, cus, 150 * 1024, ns, nm);
+            snprintf(nm, sizeof nm, "desc aligned128 16 waves/WG, 150 KB LDS, %d stream(s)", ns);
+            run(k_frames_desc_al<4, 16, 128>, 16, cus, 150 * 1024, ns, nm);
+        }
+        for (int ns : {1, 4}) {
+            const int reps = 400;
+            for (int pass = 0; pass < 2; ++pass) {
+                CHECK(hipDeviceSynchronize());
+                auto t0 = std::chrono::steady_clock::now();
+                for (int i = 0; i < reps; ++i)
+                    hipLaunchKernelGGL(k_stream<false>, dim3(cus * 2), dim3(256), 0, st[i % ns], (const u32x4*)bufs[i % NB], nbytes / 16, out);
+                CHECK(hipDeviceSynchronize());
+                const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+                if (pass) printf("stream dwordx4 grid=%dx256, %d stream(s)                %9.2f us/step  %8.1f GB/s whole job\n", cus * 2, ns, us, nbytes / (us * 1e-6) / 1e9);
+            }
         }
         return 0;
     }
