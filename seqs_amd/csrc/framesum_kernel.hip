@@ -72,6 +72,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_TILE_MAP
 #define FS_TILE_MAP 1  // first tile of a wave: 0 block-major, 1 wave-major, 2 a contiguous 1/8 per XCD
 #endif
+#ifndef FS_EARLY_TABLES
+#define FS_EARLY_TABLES 1  // the plain-table DMA right behind the descriptor loads (0: after the geometry)
+#endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio per block of rows
 #endif
@@ -1084,6 +1087,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         uint32_t len;
         if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(3);  // the preamble outranks other waves' row loops
         tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
+        if (FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
         build_region_a(tabs, lds);
         FS_STAMP(7);
         descriptors_ready<kOps>(S, len);
@@ -1094,7 +1098,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
         }
     }
-    plain_dma(tabs, lds, wave, lane);
+    if (!FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);
     bool x4 = false;
     if (first) x4 = header_dma<true>(T, frames, lds, hw, gl, lane);
     if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
@@ -1304,12 +1308,13 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         uint64_t S;
         uint32_t len;
         tile_descriptors(tile, grp0, n, offsets, lengths, S, len, fpt);
+        if (FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
         build_region_a(tabs, lds);
         descriptors_ready<kOps>(S, len);
         U.P = 0;
         if (first) tile_geometry(T, U, tile, grp0, gl0, n, S, len, frames, lds, ws, fpt);
     }
-    plain_dma(tabs, lds, wave, lane);
+    if (!FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);
     bool x4 = false;
     if (first) x4 = header_dma<false>(T, frames, lds, hw, gl0, lane);
     if (first) prefetch_unit(U, pf);
