@@ -4,7 +4,11 @@
 A "step" = one pass of the hot path (fused CRC-32 + IPv4 + TCP/UDP checksum +
 RecvEth verdict) over one batch of synthetic frames already resident in HBM.
 Default workload (BASELINE configs[1], C2): 65,536 x 1500-byte TCP frames per
-GPU; --config c3 runs the mixed 64/576/1500/9000 batch. NB >= 4 distinct
+GPU; --config c3 runs the mixed 64/576/1500/9000 batch; --config c4 the 1,048,576-frame
+global batch sharded round-robin over the ranks (strong scaling: RCCL gather of every
+step's digests to rank 0 and the de-interleave kernel there, both inside the step);
+--config c5 streams 9000-byte jumbo frames from pinned host memory through
+fs_digest_batch_multi, one context per GPU from ONE process (PCIe-inclusive, not HBM). NB >= 4 distinct
 batches (> 256 MiB in total) are rotated so the 256 MiB Infinity Cache cannot
 serve them. Multi-GPU (torchrun, one process per GPU, RCCL = torch "nccl"):
 every rank digests its own shard (weak scaling, frame i of the global batch
@@ -42,11 +46,15 @@ def parse():
     p.add_argument("--warmup", type=int, default=1000,
                    help="untimed launches first: throughput reaches its steady state only after several hundred "
                         "back-to-back launches (with 20 the timed steps measured 5-10%% lower)")
-    p.add_argument("--config", choices=["c2", "c3"], default="c2")
-    p.add_argument("--frames", type=int, default=65536, help="frames per GPU per step")
+    p.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2")
+    p.add_argument("--frames", type=int, default=None,
+                   help="frames per GPU per step (c2/c3/c5; default 65,536, c5 16,384) or of the global batch (c4; "
+                        "default 1,048,576)")
     p.add_argument("--batches", type=int, default=4, help="distinct resident batches rotated")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=1)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the all-cores CPU baseline (0 = the box's CPU share: OMP_NUM_THREADS or the "
+                        "affinity mask); the 1-thread figure is measured beside it")
     p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather (N>1 diagnostics)")
     p.add_argument("--gather-every", type=int, default=64,
                    help="N>1: each stream sends the digests + verdicts of this many of its steps to rank 0 in "
@@ -68,9 +76,21 @@ def parse():
 def make_batch(cfg: str, n: int, seed: int):
     from seqs_amd import synth
 
-    if cfg == "c2":
+    if cfg in ("c2", "c4"):
         return synth.uniform_batch(n, 1500, seed=seed)
+    if cfg == "c5":
+        return synth.uniform_batch(n, 9000, seed=seed)
     return synth.mixed_batch(n, seed=seed)
+
+
+def box_cores() -> int:
+    """The CPU share of this process: OMP_NUM_THREADS when set (16 per GPU on the box), else
+    the affinity mask."""
+    try:
+        v = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        v = 0
+    return max(1, v or len(os.sched_getaffinity(0)))
 
 
 def with_room(buf, off, ln, room: int = 4):
@@ -94,9 +114,10 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(cfg: str, seconds: float, threads: int):
+def cpu_rate(cfg: str, seconds: float, threads: int):
     """The C oracle (scalar restatement of eth/crc.go + headers.go + RecvEth gates, zlib
-    CRC-32) timed on a bounded C1-style sample: 4,096 frames of the same workload."""
+    CRC-32) timed on a bounded C1-style sample: batches of 4,096 frames of the same workload
+    (frames split over `threads` threads per batch)."""
     from oracle import coracle
 
     coracle.load()
@@ -110,15 +131,24 @@ def cpu_baseline(cfg: str, seconds: float, threads: int):
         el = time.perf_counter() - t0
         if el >= seconds and reps >= 3:
             break
-    gibs = nbytes * reps / el / GIB
+    return nbytes * reps / el / GIB, reps, nbytes, el
+
+
+def cpu_baseline(cfg: str, seconds: float, threads: int):
+    """All-cores figure (the box's CPU share) with the 1-thread figure beside it."""
+    threads = threads or box_cores()
+    what = {"c2": "1500-B TCP", "c4": "1500-B TCP", "c5": "9000-B TCP"}.get(cfg, "mixed")
+    v1, r1, nbytes, e1 = cpu_rate(cfg, seconds / 2, 1)
+    vn, rn, _, en = cpu_rate(cfg, seconds / 2, threads)
     return {
-        "value": round(gibs, 4),
+        "value": round(vn, 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{reps} x C1-style batch of 4096 {'1500-B TCP' if cfg == 'c2' else 'mixed'} frames "
-                  f"({nbytes} B) through oracle/framesum_oracle.c (CRC791 loop -O2 -fno-tree-vectorize + zlib "
-                  f"crc32), {el:.1f} s on {cpu_model()}",
+        "single_core": {"value": round(v1, 4), "unit": "GiB/s", "cores": 1},
+        "sample": f"C1-style batches of 4096 {what} frames ({nbytes} B) through oracle/framesum_oracle.c "
+                  f"(CRC791 loop -O2 -fno-tree-vectorize + zlib crc32): {rn} batches in {en:.1f} s on {threads} "
+                  f"threads, {r1} in {e1:.1f} s on 1 thread; {cpu_model()}",
     }
 
 
@@ -137,6 +167,8 @@ def load_pmc_traffic(cfg: str):
 
 def main():
     args = parse()
+    if args.config == "c5":
+        return main_c5(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world == 1:
         # started without torchrun: run ourselves under it as a child process
@@ -161,7 +193,9 @@ def main():
         dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1,
                                 init_method=f"tcp://127.0.0.1:{os.environ.get('MASTER_PORT', '29513')}")
 
-    n = args.frames
+    if args.config == "c4":
+        return main_c4(args, world, rank, local, dev)
+    n = args.frames or 65536
     engine = Engine(local)
     batches = []
     for b in range(max(1, args.batches)):
@@ -333,6 +367,11 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "frac_mode": "single stream: algorithmic bytes / average kernel duration (HIP events around K "
+                             "back-to-back launches on one stream, no overlap between launches)",
+                "frac_whole_job": round(bytes_per_batch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                "frac_whole_job_mode": f"algorithmic bytes per step / ms_per_step of the timed region ({ns} streams: "
+                                       "consecutive launches overlap each other's start and tail)",
                 "traffic": traffic,
                 "traffic_calibrated": traffic_cal,
                 "kernel": "digest_kernel",
@@ -346,6 +385,237 @@ def main():
     engine.close()
     if dist.is_initialized():
         dist.destroy_process_group()
+    return result
+
+
+def time_region(world, dist, torch, body):
+    """barrier + synchronize, body(), synchronize + barrier; max over ranks."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    body()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def main_c4(args, world, rank, local, dev):
+    """C4 (BASELINE configs[3]): one global batch of 1,048,576 x 1500-B frames per step,
+    frame i on rank i mod N (strong scaling). A step: every rank digests its shard into a
+    slab (digests + verdicts, fs_shard_slab_bytes layout), RCCL gathers the slabs to rank 0,
+    rank 0's de-interleave kernel writes the digests in global frame order. Two slots
+    alternate on two streams, so step i's gather and de-interleave overlap step i+1's kernel."""
+    import torch
+    import torch.distributed as dist
+
+    from seqs_amd import Engine, shard_count, shard_slab_bytes
+
+    n_global = args.frames or (1 << 20)
+    engine = Engine(local)
+    n = shard_count(n_global, world, rank)
+    m = (n_global + world - 1) // world
+    sb = shard_slab_bytes(n_global, world)
+    nb = 2  # 2 x 1.57 GB resident at N=1: far past the 256 MiB Infinity Cache
+    batches = []
+    for b in range(nb):
+        buf, off, ln = make_batch("c4", n, seed=1 + 1000 * rank + b)
+        batches.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)))
+    bytes_local = int(batches[0][2].cpu().numpy().astype(np.int64).sum())
+    t = torch.tensor([bytes_local], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(t)
+    bytes_global = int(t.item())
+    gather = dist.is_initialized()
+    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    # slot k: rank 0 gathers into recv[k] (world slabs back to back; its own slab is slab 0),
+    # other ranks digest into send[k]
+    recv = [torch.empty(world * sb, dtype=torch.uint8, device=dev) for _ in range(2)] if rank == 0 else None
+    send = [recv[k][:sb] for k in range(2)] if rank == 0 else \
+        [torch.empty(sb, dtype=torch.uint8, device=dev) for _ in range(2)]
+    gout = [torch.empty((n_global, 2), dtype=torch.int32, device=dev) for _ in range(2)] if rank == 0 else None
+    gst = [torch.empty(n_global, dtype=torch.uint8, device=dev) for _ in range(2)] if rank == 0 else None
+    pend = [None, None]
+
+    def views(k):
+        return send[k][: 8 * m].view(torch.int32)[: 2 * n].view(n, 2), send[k][8 * m : 8 * m + n]
+
+    def step(i):
+        k = i % 2
+        s = streams[k]
+        fb, fo, fl = batches[i % nb]
+        with torch.cuda.stream(s):
+            if pend[k] is not None:
+                pend[k].wait()  # slot k's previous gather has read send[k] (stream-side wait)
+                pend[k] = None
+            o, st = views(k)
+            engine.digest_device(fb, fo, fl, mtu=0, out=o, status=st, stream=s)
+            if gather:
+                rl = [recv[k][r * sb : (r + 1) * sb] for r in range(world)] if rank == 0 else None
+                pend[k] = dist.gather(send[k], rl, dst=0, async_op=True)
+            if rank == 0:
+                if pend[k] is not None:
+                    pend[k].wait()
+                    pend[k] = None
+                engine.deinterleave_device(recv[k], world, n_global, out=gout[k], status=gst[k], stream=s)
+
+    def drain():
+        for k in range(2):
+            if pend[k] is not None:
+                with torch.cuda.stream(streams[k]):
+                    pend[k].wait()
+                pend[k] = None
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
+    torch.cuda.synchronize()
+
+    def body():
+        for i in range(args.steps):
+            step(args.warmup + i)
+        drain()
+
+    elapsed = time_region(world, dist, torch, body)
+
+    # check on rank 0: the last step's global-order output is the interleave of the slabs
+    # gathered for it (the de-interleave and the gather layout), and rank 0's own frames
+    if rank == 0:
+        k = (args.warmup + args.steps - 1) % 2
+        torch.cuda.synchronize()
+        g = recv[k].cpu().numpy()
+        i = np.arange(n_global)
+        r, j = i % world, i // world
+        exp_w = np.stack([g[r * sb + 8 * j + b] for b in range(8)], axis=1).view(np.int32).reshape(n_global, 2)
+        assert np.array_equal(gout[k].cpu().numpy(), exp_w), "de-interleave mismatch"
+        assert np.array_equal(gst[k].cpu().numpy(), g[r * sb + 8 * m + j]), "de-interleave verdict mismatch"
+        assert (gst[k].cpu().numpy() == 0).all(), "valid frames must all verify"
+
+    # kernel-only: K back-to-back shard digests on one stream (events on the launch stream)
+    k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = streams[0]
+    with torch.cuda.stream(ms):
+        k0.record(ms)
+        for i in range(args.steps):
+            fb, fo, fl = batches[i % nb]
+            o, st = views(0)
+            engine.digest_device(fb, fo, fl, mtu=0, out=o, status=st, stream=ms)
+        k1.record(ms)
+    torch.cuda.synchronize()
+    k_ms = k0.elapsed_time(k1) / args.steps
+    t = torch.tensor([k_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    k_ms_max = float(t.item())
+    value = bytes_global * args.steps / elapsed / GIB
+    if rank == 0:
+        result = {
+            "metric": "GiB/s device-resident CRC-32+Internet-csum over batched MTU frames; % HBM peak",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic: {nb} distinct resident shard batches per rank of valid 1500-B TCP frames, rotated",
+            "config": {
+                "workload": f"C4: {n_global}-frame global batch of 1500-B frames sharded round-robin over {world} "
+                            "GPU(s) (BASELINE configs[3])",
+                "global_batch_frames": n_global,
+                "bytes_per_step": bytes_global,
+                "parallelism": f"frame i on rank i mod {world}; per step: shard digest, RCCL gather of the digests + "
+                               "verdicts to rank 0, de-interleave kernel on rank 0 (all inside the step)"
+                if world > 1 else "single GPU: shard = whole batch; de-interleave kernel inside the step",
+                "kernel_only_gibs": round(bytes_global / (k_ms_max * 1e-3) / GIB, 3),
+                "kernel_only_ms": round(k_ms_max, 5),
+                "streams": 2,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(bytes_local / (k_ms * 1e-3) / 1e9, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(bytes_local / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "kernel": "digest_kernel",
+                "kernel_avg_us": round(k_ms * 1e3, 3),
+                "frac_mode": "rank 0's shard kernel, single stream",
+            },
+            "cpu_baseline": cpu_baseline("c4", args.cpu_seconds, args.cpu_threads)
+            if world == 1 and args.cpu_seconds > 0 else None,
+        }
+        print(json.dumps(result), flush=True)
+    engine.close()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def main_c5(args):
+    """C5 (BASELINE configs[4]): 9000-B jumbo frames streamed from pinned host memory to
+    --gpus GPUs from ONE process: fs_digest_batch_multi, one context per GPU, byte-balanced
+    contiguous blocks, each on its own host thread with its own H2D / kernel / D2H pipeline.
+    A step = one call over the whole host batch (results back in host memory). Bound by PCIe
+    and host memory, not HBM."""
+    import torch
+
+    from seqs_amd import Engine, digest_host_multi
+
+    ngpu = max(1, args.gpus)
+    per_gpu = args.frames or 16384
+    engines = [Engine(d) for d in range(ngpu)]
+    n = per_gpu * ngpu
+    src, off, ln = make_batch("c5", n, seed=55)
+    pinned = engines[0].host_empty(src.shape, np.uint8)
+    pinned[:] = src
+    del src
+    total = int(ln.astype(np.int64).sum())
+    for _ in range(max(1, args.warmup)):
+        digest_host_multi(engines, pinned, off, ln)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, st = digest_host_multi(engines, pinned, off, ln)
+    elapsed = time.perf_counter() - t0
+    assert (st == 0).all(), "valid frames must all verify"
+    value = total * args.steps / elapsed / GIB
+    result = {
+        "metric": "GiB/s end-to-end (pinned host memory -> GPU -> host) CRC-32+Internet-csum over batched jumbo frames",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": ngpu,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": f"synthetic: one pinned host batch of {n} valid 9000-B TCP frames ({total / 1e9:.2f} GB)",
+        "config": {
+            "workload": f"C5: {per_gpu} x 9000-B jumbo frames per GPU streamed from pinned host memory "
+                        "(BASELINE configs[4]); PCIe-inclusive, not the HBM metric",
+            "frames_per_gpu": per_gpu,
+            "bytes_per_step": total,
+            "parallelism": f"fs_digest_batch_multi over {ngpu} context(s), one per GPU, one host process",
+        },
+        "roofline": {"bound": "pcie", "peak": 63.0 * ngpu, "unit": "GB/s",
+                     "achieved": round(total / (elapsed / args.steps) / 1e9, 2),
+                     "frac": round(total / (elapsed / args.steps) / 1e9 / (63.0 * ngpu), 4),
+                     "kernel": None, "note": "PCIe Gen5 x16 spec 63 GB/s per GPU (MI355X_MICROARCH.md)"},
+        "cpu_baseline": cpu_baseline("c5", args.cpu_seconds, args.cpu_threads) if args.cpu_seconds > 0 else None,
+    }
+    print(json.dumps(result), flush=True)
+    for e in engines:
+        e.close()
     return result
 
 

@@ -1,0 +1,271 @@
+//go:build framesum
+
+// Package eth addition: the batched, GPU-side form of the checksum work that
+// stacks.PortStack.RecvEth and the TX header builders do one frame at a time.
+//
+// Drop this file into soypat/seqs/eth/ and build with `-tags framesum` next to
+// libframesum.so (include/framesum.h of the framesum engine). The existing
+// per-frame functions -- CRC791 (crc.go:13-84), (*IPv4Header).CalculateChecksum
+// (headers.go:333), (*UDPHeader).CalculateChecksumIPv4 (:382) and
+// (*TCPHeader).CalculateChecksumIPv4 (:510) -- stay untouched and remain the
+// parity reference: for every frame, DigestBatch returns exactly the L4 checksum
+// RecvEth computes (`gotsum`, stacks/portstack.go:239 / :303), the IPv4 header
+// checksum of frame[14:34], the IEEE 802.3 CRC-32 of the frame, and the error
+// class RecvEth would return (Verdict).
+//
+// Not compiled in the framesum repository (its build image has no Go toolchain);
+// tests/csrc/go_binding_replay.c replays DigestBatch's packing and calls through
+// the same C ABI on the GPU and is checked against the CPU oracle.
+package eth
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../third_party/framesum/include
+#cgo LDFLAGS: -L${SRCDIR}/../third_party/framesum/lib -lframesum -Wl,-rpath,${SRCDIR}/../third_party/framesum/lib
+#include <framesum.h>
+#include <stdlib.h>
+*/
+import "C"
+
+import (
+	"errors"
+	"unsafe"
+)
+
+// Digest is the per-frame result of DigestBatch. Its layout is C struct fs_digest.
+type Digest struct {
+	CRC32  uint32 // IEEE 802.3 CRC-32 of frame[0:len)
+	IPCsum uint16 // (*IPv4Header).CalculateChecksum() of frame[14:34]; 0 if the frame is shorter
+	L4Csum uint16 // the TCP/UDP checksum RecvEth computes; 0 when RecvEth rejects the frame earlier
+}
+
+// Verdict is the error class RecvEth returns for a frame (enum fs_verdict), under the
+// engine's stack model: MTU as passed, no MAC / IP destination filter, sockets open for
+// both protocols. stacks.PortStack.RecvEthBatch applies the remaining policy.
+type Verdict uint8
+
+const (
+	VerdictOK                 Verdict = 0  // checksum verified
+	VerdictPacketSmol         Verdict = 1  // errPacketSmol
+	VerdictExceedsMTU         Verdict = 2  // errPacketExceedsMTU
+	VerdictNotIPv4            Verdict = 3  // ignored: neither IPv4 nor ARP
+	VerdictARP                Verdict = 4  // ARP frame
+	VerdictIPVersion          Verdict = 5  // errIPVersion
+	VerdictInvalidIHL         Verdict = 6  // errInvalidIHL
+	VerdictBadIPTotalLenOrIHL Verdict = 7  // errBadIPTotalLenOrIHL
+	VerdictUnknownIPProto     Verdict = 8  // errUnknownIPProto
+	VerdictTooShortTCPOrUDP   Verdict = 9  // errTooShortTCPOrUDP
+	VerdictZeroPort           Verdict = 10 // errZeroPort
+	VerdictBadUDPLength       Verdict = 11 // errBadUDPLength
+	VerdictBadTCPOffset       Verdict = 12 // errBadTCPOffset
+	VerdictChecksum           Verdict = 13 // ErrChecksumTCPorUDP
+	VerdictFCS                Verdict = 14 // DigestBatchFCS only: FCS missing or wrong
+)
+
+// The C struct and this one must agree byte for byte (8 bytes, no padding).
+var _ [8]byte = [unsafe.Sizeof(Digest{})]byte{}
+
+// GPU is one framesum context on one device: device CRC tables, staging buffers and
+// pinned memory for the frames. Like PortStack, it is not safe for concurrent use.
+type GPU struct {
+	ctx  *C.fs_ctx
+	pin  unsafe.Pointer // pinned staging buffer (fs_host_alloc)
+	pcap int
+	offs []uint64
+	lens []uint32
+}
+
+// OpenGPU creates a context on HIP device `device` (an MI355X, gfx950).
+func OpenGPU(device int) (*GPU, error) {
+	var ctx *C.fs_ctx
+	if st := C.fs_ctx_create(C.int(device), &ctx); st != C.FS_SUCCESS {
+		return nil, errors.New("framesum: " + C.GoString(C.fs_last_error(nil)))
+	}
+	return &GPU{ctx: ctx}, nil
+}
+
+// Close releases the context and its pinned staging memory.
+func (g *GPU) Close() error {
+	if g.ctx == nil {
+		return nil
+	}
+	if g.pin != nil {
+		C.fs_host_free(g.ctx, g.pin)
+		g.pin, g.pcap = nil, 0
+	}
+	C.fs_ctx_destroy(g.ctx)
+	g.ctx = nil
+	return nil
+}
+
+func (g *GPU) lastErr() error { return errors.New("framesum: " + C.GoString(C.fs_last_error(g.ctx))) }
+
+// stage packs frames back to back, each at a 4-byte aligned offset, into pinned memory,
+// followed by 16 spare bytes (the engine may read up to 3 bytes past a frame's end). The
+// copies run on the host; the device reads the pinned buffer over PCIe in chunks that
+// overlap its kernels (fs_digest_batch_host).
+func (g *GPU) stage(frames [][]byte, spare int) ([]byte, error) {
+	n := len(frames)
+	if cap(g.offs) < n {
+		g.offs = make([]uint64, n)
+		g.lens = make([]uint32, n)
+	}
+	g.offs, g.lens = g.offs[:n], g.lens[:n]
+	total := 0
+	for i, f := range frames {
+		g.offs[i] = uint64(total)
+		g.lens[i] = uint32(len(f))
+		total += (len(f) + spare + 3) &^ 3
+	}
+	total += 16
+	if total > g.pcap {
+		if g.pin != nil {
+			C.fs_host_free(g.ctx, g.pin)
+			g.pin, g.pcap = nil, 0
+		}
+		var p unsafe.Pointer
+		if st := C.fs_host_alloc(g.ctx, C.uint64_t(total), &p); st != C.FS_SUCCESS {
+			return nil, g.lastErr()
+		}
+		g.pin, g.pcap = p, total
+	}
+	buf := unsafe.Slice((*byte)(g.pin), total)
+	for i, f := range frames {
+		copy(buf[g.offs[i]:], f)
+	}
+	return buf, nil
+}
+
+// DigestBatch computes, for every frame, the digest and the RecvEth verdict (mtu as
+// PortStack's MTU; 0 disables the MTU gates). out and verdicts must hold len(frames).
+func (g *GPU) DigestBatch(frames [][]byte, mtu uint16, out []Digest, verdicts []Verdict) error {
+	n := len(frames)
+	if len(out) < n || len(verdicts) < n {
+		return errors.New("framesum: output slices too short")
+	}
+	if n == 0 {
+		return nil
+	}
+	buf, err := g.stage(frames, 0)
+	if err != nil {
+		return err
+	}
+	st := C.fs_digest_batch_host(g.ctx, (*C.uint8_t)(unsafe.Pointer(&buf[0])), C.uint64_t(len(buf)),
+		(*C.uint64_t)(unsafe.Pointer(&g.offs[0])), (*C.uint32_t)(unsafe.Pointer(&g.lens[0])),
+		C.uint32_t(n), C.uint32_t(mtu), (*C.fs_digest)(unsafe.Pointer(&out[0])),
+		(*C.uint8_t)(unsafe.Pointer(&verdicts[0])))
+	if st != C.FS_SUCCESS {
+		return g.lastErr()
+	}
+	return nil
+}
+
+// FillBatch is the checksum part of the TX header builders for many frames at once
+// (stacks/port_tcp.go:178, :193; dhcp_client.go:479, :486): it writes the IPv4 header
+// checksum and the TCP/UDP checksum into every frame RecvEth would checksum, in place
+// in frames, and with appendFCS the CRC-32 little-endian after each frame (each frame
+// slice must then have 4 bytes of capacity past its length). out / verdicts receive
+// what DigestBatch reports for the frames as written.
+func (g *GPU) FillBatch(frames [][]byte, mtu uint16, appendFCS bool, out []Digest, verdicts []Verdict) error {
+	n := len(frames)
+	if len(out) < n || len(verdicts) < n {
+		return errors.New("framesum: output slices too short")
+	}
+	if n == 0 {
+		return nil
+	}
+	spare, flags := 0, C.uint32_t(C.FS_FILL_CSUM)
+	if appendFCS {
+		spare, flags = 4, flags|C.FS_FCS_APPEND
+		for _, f := range frames {
+			if cap(f)-len(f) < 4 {
+				return errors.New("framesum: FillBatch with appendFCS needs 4 bytes of capacity past each frame")
+			}
+		}
+	}
+	buf, err := g.stage(frames, spare)
+	if err != nil {
+		return err
+	}
+	st := C.fs_fill_batch_host(g.ctx, (*C.uint8_t)(unsafe.Pointer(&buf[0])), C.uint64_t(len(buf)),
+		(*C.uint64_t)(unsafe.Pointer(&g.offs[0])), (*C.uint32_t)(unsafe.Pointer(&g.lens[0])),
+		C.uint32_t(n), C.uint32_t(mtu), flags, (*C.fs_digest)(unsafe.Pointer(&out[0])),
+		(*C.uint8_t)(unsafe.Pointer(&verdicts[0])))
+	if st != C.FS_SUCCESS {
+		return g.lastErr()
+	}
+	for i, f := range frames {
+		copy(f[:len(f)+spare], buf[g.offs[i]:g.offs[i]+uint64(len(f)+spare)])
+	}
+	return nil
+}
+
+// GPUs is one host process's set of contexts, one per GPU, for NIC rings larger than one
+// PCIe link carries (fs_digest_batch_multi; BASELINE configs[4]).
+type GPUs struct {
+	gpus []*GPU
+	ctxs unsafe.Pointer // C array of fs_ctx* (cgo: Go memory may not hold C pointers passed to C)
+	buf  *GPU           // stages the frames (its pinned buffer)
+}
+
+// OpenGPUs opens one context per listed device.
+func OpenGPUs(devices []int) (*GPUs, error) {
+	if len(devices) == 0 {
+		return nil, errors.New("framesum: no devices")
+	}
+	m := &GPUs{ctxs: C.malloc(C.size_t(len(devices)) * C.size_t(unsafe.Sizeof(uintptr(0))))}
+	arr := unsafe.Slice((**C.fs_ctx)(m.ctxs), len(devices))
+	for i, d := range devices {
+		g, err := OpenGPU(d)
+		if err != nil {
+			m.Close()
+			return nil, err
+		}
+		m.gpus = append(m.gpus, g)
+		arr[i] = g.ctx
+	}
+	m.buf = m.gpus[0]
+	return m, nil
+}
+
+// Close releases every context.
+func (m *GPUs) Close() error {
+	for _, g := range m.gpus {
+		g.Close()
+	}
+	m.gpus = nil
+	if m.ctxs != nil {
+		C.free(m.ctxs)
+		m.ctxs = nil
+	}
+	return nil
+}
+
+// DigestBatch spreads the batch over the contexts: byte-balanced runs of frames, each on
+// its own GPU, PCIe link and host thread; results in batch order.
+func (m *GPUs) DigestBatch(frames [][]byte, mtu uint16, out []Digest, verdicts []Verdict) error {
+	n := len(frames)
+	if len(out) < n || len(verdicts) < n {
+		return errors.New("framesum: output slices too short")
+	}
+	if n == 0 {
+		return nil
+	}
+	buf, err := m.buf.stage(frames, 0)
+	if err != nil {
+		return err
+	}
+	g := m.buf
+	st := C.fs_digest_batch_multi((**C.fs_ctx)(m.ctxs), C.int(len(m.gpus)), (*C.uint8_t)(unsafe.Pointer(&buf[0])),
+		C.uint64_t(len(buf)), (*C.uint64_t)(unsafe.Pointer(&g.offs[0])), (*C.uint32_t)(unsafe.Pointer(&g.lens[0])),
+		C.uint32_t(n), C.uint32_t(mtu), (*C.fs_digest)(unsafe.Pointer(&out[0])),
+		(*C.uint8_t)(unsafe.Pointer(&verdicts[0])))
+	if st != C.FS_SUCCESS {
+		for _, x := range m.gpus {
+			if msg := C.GoString(C.fs_last_error(x.ctx)); msg != "" {
+				return errors.New("framesum: " + msg)
+			}
+		}
+		return errors.New("framesum: fs_digest_batch_multi failed")
+	}
+	return nil
+}

@@ -161,12 +161,58 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
  * block k runs on ctxs[k] (one context per GPU; several contexts may share a GPU), every
  * block at once, each on its own host thread with its own H2D / kernel / D2H pipeline.
  * A block's digests and verdicts are copied straight into out/status at the block's own
- * indices: the host arrays are the gather, so no device collective is involved.
+ * indices: the host arrays are the gather, so no device collective is involved (the
+ * device-resident RCCL form is fs_digest_batch_sharded below).
+ * Blocks are runs of frames in BUFFER order: when the offsets are not non-decreasing, the
+ * frames are first ordered by offset, so each context still copies only its own bytes.
  * ctxs must be distinct. Returns when every block is done; on failure, the status of the
- * lowest failing block, whose message is in fs_last_error of that block's context. */
+ * lowest failing block, whose message is in fs_last_error of that block's context (every
+ * entry point clears its context's message first, so only failing contexts hold one). */
 fs_status fs_digest_batch_multi(fs_ctx* const* ctxs, int nctx, const uint8_t* frames, uint64_t frames_bytes,
                                 const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint32_t mtu,
                                 fs_digest* out, uint8_t* status);
+
+/* ---- Device-resident multi-GPU form with RCCL (BASELINE configs[3], C4; SURVEY.md §8b
+ * "N GPUs + RCCL gather", §8e). Replaces the same per-frame calls as fs_digest_batch
+ * (stacks/portstack.go:163 RecvEth -> :240 / :303 CalculateChecksumIPv4) for a batch held
+ * in the HBM of several GPUs of one node, driven from ONE host process (a Go PortStack):
+ * frames are independent (eth/crc.go:12-17, CRC791 is per call), so the batch shards with
+ * no data-path collective, and RCCL over xGMI is used only to gather the 8-byte digests and
+ * 1-byte verdicts back to the first device.
+ *
+ * A group holds one context, one stream and one RCCL communicator (ncclCommInitAll) per
+ * device; devices must be distinct. */
+typedef struct fs_group fs_group;
+fs_status fs_group_create(const int* devices, int ndev, fs_group** out);
+fs_status fs_group_destroy(fs_group* g);
+/* Message for the last failing call on `g` (or of fs_group_create when g is NULL). */
+const char* fs_group_last_error(const fs_group* g);
+
+/* Round-robin sharding of a global batch of n frames over nshards shards: global frame i
+ * is local frame i / nshards of shard i % nshards; shard k holds fs_shard_count(n, nshards, k)
+ * frames. */
+uint64_t fs_shard_count(uint64_t n, uint32_t nshards, uint32_t shard);
+
+/* Digest a global batch sharded round-robin over the group's devices. frames[k], offsets[k],
+ * lengths[k] are DEVICE pointers on the group's k-th device describing shard k (its
+ * fs_shard_count(n, ndev, k) frames, laid out as fs_digest_batch expects). Every shard's
+ * kernel runs on its own device at once; the digests and verdicts are then gathered to the
+ * first device with ncclGather and put back in global frame order there by a de-interleave
+ * kernel: out (n digests) and status (n bytes, nullable) are DEVICE pointers on the group's
+ * first device. Returns when they are written. At most 2^31 frames per shard. */
+fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, const uint64_t* const* offsets,
+                                  const uint32_t* const* lengths, uint64_t n, uint32_t mtu, fs_digest* out,
+                                  uint8_t* status);
+
+/* The de-interleave step alone, for callers that gather the shards themselves (one process
+ * per GPU, e.g. torch.distributed over RCCL): `gathered` (device memory of ctx's device)
+ * holds nshards slabs back to back; slab k is shard k's m = ceil(n / nshards) digests (8 B
+ * each) followed by its m verdict bytes, padded to a multiple of 256 bytes:
+ * fs_shard_slab_bytes(n, nshards) bytes per slab. Writes out[i] / status[i] (nullable) for
+ * global frames i < n. Asynchronous on `stream`. */
+uint64_t fs_shard_slab_bytes(uint64_t n, uint32_t nshards);
+fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards, uint64_t n, fs_digest* out,
+                          uint8_t* status, void* stream);
 
 /* Kernel variant of a context's launches. The engine has two: a one-pass kernel
  * for batches of similar frame lengths, and one that splits long frames into

@@ -14,10 +14,13 @@ from .framesum import (  # noqa: F401
     Digest,
     Engine,
     FramesumError,
+    Group,
     digest_host_multi,
     lib_path,
     load_library,
     pack_frames,
+    shard_count,
+    shard_slab_bytes,
     split_digests,
 )
 
@@ -31,9 +34,12 @@ __all__ = [
     "Digest",
     "Engine",
     "FramesumError",
+    "Group",
     "digest_host_multi",
     "lib_path",
     "load_library",
     "pack_frames",
+    "shard_count",
+    "shard_slab_bytes",
     "split_digests",
 ]

@@ -6,12 +6,14 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <system_error>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/framesum.h"
 #include "framesum_internal.h"
+#include "framesum_plan.h"
 
 using framesum::FsTables;
 
@@ -183,6 +185,7 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
 
 fs_status fs_ctx_destroy(fs_ctx* ctx) {
     if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
     (void)hipSetDevice(ctx->device);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
     if (ctx->compute_stream) (void)hipStreamSynchronize(ctx->compute_stream);
@@ -209,6 +212,7 @@ const char* fs_last_error(const fs_ctx* ctx) { return ctx ? ctx->err.c_str() : g
 fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths,
                           uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status, void* stream) {
     if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
     if (n == 0) return FS_SUCCESS;
     if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_digest_batch: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_digest_batch: null pointer");
@@ -224,6 +228,7 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
 fs_status fs_fill_batch(fs_ctx* ctx, uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                         uint32_t mtu, uint32_t flags, fs_digest* out, uint8_t* status, void* stream) {
     if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
     if (flags & ~(uint32_t)(FS_FILL_CSUM | FS_FCS_APPEND)) return set_err(ctx, FS_E_INVALID, "fs_fill_batch: unknown flags");
     if (n == 0) return FS_SUCCESS;
     if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_fill_batch: n too large (at most 2^31 frames per call)");
@@ -240,6 +245,7 @@ fs_status fs_fill_batch(fs_ctx* ctx, uint8_t* frames, const uint64_t* offsets, c
 fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths,
                               uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status, void* stream) {
     if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
     if (n == 0) return FS_SUCCESS;
     if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_fcs: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_fcs: null pointer");
@@ -255,10 +261,14 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status) {
     if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
     if (n == 0) return FS_SUCCESS;
     if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: null pointer");
+    const uint32_t bad = framesum::plan::first_frame_out_of_range(offsets, lengths, n, frames_bytes);
+    if (bad < n)
+        return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(bad) + " ends past frames_bytes");
     FS_HIP(ctx, hipSetDevice(ctx->device));
     FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));  // the pinned mirrors are free
     fs_status pst = ensure_pinned(ctx, n);
@@ -269,42 +279,20 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     uint8_t* h_st = ctx->h_pin + (size_t)n * 20;
     std::memcpy(h_off, offsets, (size_t)n * 8);
     std::memcpy(h_len, lengths, (size_t)n * 4);
-    uint32_t c0 = 0;
-    for (int chunk = 0; c0 < n; ++chunk) {
-        // frames [c0, c1): grow while the byte span [lo, hi) stays within kChunkBytes
-        uint64_t lo = offsets[c0], hi = offsets[c0] + lengths[c0];
-        uint32_t c1 = c0 + 1;
-        while (c1 < n && c1 - c0 < kChunkFrames) {
-            const uint64_t o = offsets[c1], e = o + lengths[c1];
-            const uint64_t nlo = o < lo ? o : lo, nhi = e > hi ? e : hi;
-            if (nhi - nlo > kChunkBytes) break;
-            lo = nlo;
-            hi = nhi;
-            ++c1;
-        }
-        if (c1 < n && c1 - c0 < 64 && hi - lo < kChunkBytes / 4) {
-            // the next frame lies far away (frames not stored in index order): one chunk
-            // spanning the rest of the batch instead of a launch per handful of frames
-            for (; c1 < n; ++c1) {
-                const uint64_t o = offsets[c1], e = o + lengths[c1];
-                lo = o < lo ? o : lo;
-                hi = e > hi ? e : hi;
-            }
-        }
-        for (uint32_t i = c0; i < c1; ++i)
-            if (offsets[i] + lengths[i] > frames_bytes)
-                return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(i) +
-                                                      " ends past frames_bytes");
-        // copy [cpy_lo, cpy_hi): 16-B aligned start with a 16-B prefix (sub-4-byte frames read
-        // up to 12 bytes before their start), end rounded up to the dword the engine may read
-        const uint64_t cpy_lo = (lo >= 16 ? lo - 16 : 0) & ~uint64_t(15);
-        uint64_t cpy_hi = (hi + 3) & ~uint64_t(3);
-        if (cpy_hi > frames_bytes) cpy_hi = frames_bytes;
+    std::vector<framesum::plan::Chunk> chunks;
+    try {
+        framesum::plan::host_chunks(offsets, lengths, n, frames_bytes, kChunkBytes, kChunkFrames, chunks);
+    } catch (const std::bad_alloc&) {
+        return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: out of host memory");
+    }
+    for (size_t chunk = 0; chunk < chunks.size(); ++chunk) {
+        const uint32_t c0 = chunks[chunk].c0, c1 = chunks[chunk].c1;
+        const uint64_t cpy_lo = chunks[chunk].cpy_lo, cpy_hi = chunks[chunk].cpy_hi;
         HostSlot& sl = ctx->slot[chunk % kHostSlots];
         const uint32_t cnt = c1 - c0;
         fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, cnt);
         if (st != FS_SUCCESS) return st;
-        hipStream_t cs = ctx->copy_stream, ks = ctx->compute_stream;
+        const hipStream_t cs = ctx->copy_stream, ks = ctx->compute_stream;
         if (sl.used) FS_HIP(ctx, hipStreamWaitEvent(cs, sl.consumed, 0));  // chunk c - kHostSlots done with it
         FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, cs));
         FS_HIP(ctx, hipMemcpyAsync(sl.d_offsets, h_off + c0, (size_t)cnt * 8, hipMemcpyHostToDevice, cs));
@@ -320,7 +308,6 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         sl.used = true;
         FS_HIP(ctx, hipMemcpyAsync(h_out + c0, sl.d_out, (size_t)cnt * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
         if (status) FS_HIP(ctx, hipMemcpyAsync(h_st + c0, sl.d_status, cnt, hipMemcpyDeviceToHost, ks));
-        c0 = c1;
     }
     FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));
     std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
@@ -332,6 +319,7 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
                              const uint32_t* lengths, uint32_t n, uint32_t mtu, uint32_t flags, fs_digest* out,
                              uint8_t* status) {
     if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
     if (flags & ~(uint32_t)(FS_FILL_CSUM | FS_FCS_APPEND))
         return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: unknown flags");
     if (n == 0) return FS_SUCCESS;
@@ -339,12 +327,13 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
     if (!frames || !offsets || !lengths || !out) return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: null pointer");
     // One staged span [lo, hi) (the frames and, with FS_FCS_APPEND, their FCS bytes), copied in,
     // filled, copied back. Not chunk-pipelined: written spans of unordered batches may interleave.
-    const uint64_t extra = (flags & FS_FCS_APPEND) ? 4u : 0u;
+    const uint32_t extra = (flags & FS_FCS_APPEND) ? 4u : 0u;
+    const uint32_t bad = framesum::plan::first_frame_out_of_range(offsets, lengths, n, frames_bytes, extra);
+    if (bad < n)
+        return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: frame " + std::to_string(bad) + " ends past frames_bytes");
     uint64_t lo = UINT64_MAX, hi = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint64_t o = offsets[i], e = o + lengths[i] + extra;
-        if (e > frames_bytes)
-            return set_err(ctx, FS_E_INVALID, "fs_fill_batch_host: frame " + std::to_string(i) + " ends past frames_bytes");
         lo = o < lo ? o : lo;
         hi = e > hi ? e : hi;
     }
@@ -358,9 +347,8 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
     uint8_t* h_st = ctx->h_pin + (size_t)n * 20;
     std::memcpy(h_off, offsets, (size_t)n * 8);
     std::memcpy(h_len, lengths, (size_t)n * 4);
-    const uint64_t cpy_lo = (lo >= 16 ? lo - 16 : 0) & ~uint64_t(15);
-    uint64_t cpy_hi = (hi + 3) & ~uint64_t(3);
-    if (cpy_hi > frames_bytes) cpy_hi = frames_bytes;
+    uint64_t cpy_lo, cpy_hi;
+    framesum::plan::copy_span(lo, hi, frames_bytes, cpy_lo, cpy_hi);
     HostSlot& sl = ctx->slot[0];
     fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, n);
     if (st != FS_SUCCESS) return st;
@@ -390,6 +378,7 @@ fs_status fs_digest_batch_multi(fs_ctx* const* ctxs, int nctx, const uint8_t* fr
     if (!ctxs || nctx <= 0) return FS_E_INVALID;
     for (int k = 0; k < nctx; ++k) {
         if (!ctxs[k]) return FS_E_INVALID;
+        ctxs[k]->err.clear();
         for (int j = 0; j < k; ++j)
             if (ctxs[j] == ctxs[k])
                 return set_err(ctxs[k], FS_E_INVALID, "fs_digest_batch_multi: a context appears twice in ctxs");
@@ -399,39 +388,98 @@ fs_status fs_digest_batch_multi(fs_ctx* const* ctxs, int nctx, const uint8_t* fr
         return set_err(ctxs[0], FS_E_INVALID, "fs_digest_batch_multi: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out)
         return set_err(ctxs[0], FS_E_INVALID, "fs_digest_batch_multi: null pointer");
-    // block k = frames [cut[k], cut[k+1]): the first frame whose running byte count reaches
-    // k/nctx of the total starts block k (contiguous blocks: one H2D stream per GPU)
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; ++i) total += lengths[i];
-    std::vector<uint32_t> cut(nctx + 1, n);
-    cut[0] = 0;
-    {
-        uint64_t run = 0;
-        int k = 1;
-        for (uint32_t i = 0; i < n && k < nctx; ++i) {
-            while (k < nctx && (unsigned __int128)run * nctx >= (unsigned __int128)total * k) cut[k++] = i;
-            run += lengths[i];
+    const uint32_t bad = framesum::plan::first_frame_out_of_range(offsets, lengths, n, frames_bytes);
+    if (bad < n)
+        return set_err(ctxs[0], FS_E_INVALID, "fs_digest_batch_multi: frame " + std::to_string(bad) + " ends past frames_bytes");
+    // block k = a run of frames in buffer order holding about 1/nctx of the bytes (one H2D
+    // stream per GPU over its own bytes); unordered batches are ordered by offset first and
+    // their results scattered back to batch order
+    framesum::plan::MultiPlan plan;
+    struct Block {
+        std::vector<uint64_t> off;
+        std::vector<uint32_t> len;
+        std::vector<fs_digest> dig;
+        std::vector<uint8_t> st;
+    };
+    std::vector<Block> blk;
+    std::vector<fs_status> st;
+    try {
+        framesum::plan::multi_blocks(offsets, lengths, n, nctx, plan);
+        blk.resize(nctx);
+        st.assign(nctx, FS_SUCCESS);
+        if (!plan.order.empty()) {
+            for (int k = 0; k < nctx; ++k) {
+                Block& b = blk[k];
+                const uint32_t p0 = plan.cut[k], p1 = plan.cut[k + 1];
+                b.off.resize(p1 - p0);
+                b.len.resize(p1 - p0);
+                b.dig.resize(p1 - p0);
+                b.st.resize(status ? p1 - p0 : 0);
+                for (uint32_t p = p0; p < p1; ++p) {
+                    b.off[p - p0] = offsets[plan.order[p]];
+                    b.len[p - p0] = lengths[plan.order[p]];
+                }
+            }
+        }
+    } catch (const std::bad_alloc&) {
+        return set_err(ctxs[0], FS_E_NOMEM, "fs_digest_batch_multi: out of host memory");
+    }
+    auto run_block = [&](int k) {
+        const uint32_t p0 = plan.cut[k], p1 = plan.cut[k + 1];
+        if (p1 <= p0) return;
+        if (plan.order.empty()) {
+            st[k] = fs_digest_batch_host(ctxs[k], frames, frames_bytes, offsets + p0, lengths + p0, p1 - p0, mtu,
+                                         out + p0, status ? status + p0 : nullptr);
+            return;
+        }
+        Block& b = blk[k];
+        st[k] = fs_digest_batch_host(ctxs[k], frames, frames_bytes, b.off.data(), b.len.data(), p1 - p0, mtu,
+                                     b.dig.data(), status ? b.st.data() : nullptr);
+        if (st[k] != FS_SUCCESS) return;
+        for (uint32_t p = p0; p < p1; ++p) {
+            out[plan.order[p]] = b.dig[p - p0];
+            if (status) status[plan.order[p]] = b.st[p - p0];
+        }
+    };
+    // One host thread per block beyond the first; if a thread cannot be started, its block runs
+    // on the calling thread instead (never an exception across the ABI, no joinable thread left).
+    std::vector<std::thread> workers;
+    std::vector<int> inline_blocks;
+    try {
+        workers.reserve(nctx - 1);
+        inline_blocks.reserve(nctx);
+    } catch (const std::bad_alloc&) {
+        return set_err(ctxs[0], FS_E_NOMEM, "fs_digest_batch_multi: out of host memory");
+    }
+    for (int k = 1; k < nctx; ++k) {
+        try {
+            workers.emplace_back(run_block, k);
+        } catch (const std::system_error&) {
+            inline_blocks.push_back(k);
         }
     }
-    std::vector<fs_status> st(nctx, FS_SUCCESS);
-    auto run_block = [&](int k) {
-        const uint32_t b0 = cut[k], b1 = cut[k + 1];
-        if (b1 > b0)
-            st[k] = fs_digest_batch_host(ctxs[k], frames, frames_bytes, offsets + b0, lengths + b0, b1 - b0, mtu,
-                                         out + b0, status ? status + b0 : nullptr);
-    };
-    std::vector<std::thread> workers;
-    workers.reserve(nctx - 1);
-    for (int k = 1; k < nctx; ++k) workers.emplace_back(run_block, k);
     run_block(0);
+    for (int k : inline_blocks) run_block(k);
     for (auto& w : workers) w.join();
     for (int k = 0; k < nctx; ++k)
         if (st[k] != FS_SUCCESS) return st[k];
     return FS_SUCCESS;
 }
 
+fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards, uint64_t n, fs_digest* out,
+                          uint8_t* status, void* stream) {
+    if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
+    if (n == 0) return FS_SUCCESS;
+    if (!gathered || !out || nshards == 0) return set_err(ctx, FS_E_INVALID, "fs_deinterleave: null pointer or no shards");
+    FS_HIP(ctx, hipSetDevice(ctx->device));
+    FS_HIP(ctx, framesum::launch_deinterleave(gathered, nshards, n, out, status, reinterpret_cast<hipStream_t>(stream)));
+    return FS_SUCCESS;
+}
+
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
     if (variant < 0 || variant > 2) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0, 1 or 2");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
@@ -447,6 +495,7 @@ fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out) {
 
 fs_status fs_host_free(fs_ctx* ctx, void* p) {
     if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
     if (p) FS_HIP(ctx, hipHostFree(p));
     return FS_SUCCESS;
 }

@@ -1,0 +1,197 @@
+// framesum multi-GPU group (include/framesum.h: fs_group_*, fs_digest_batch_sharded): one host
+// process drives every GPU of a node. Each device digests its round-robin shard with the
+// gfx950 kernel (through fs_digest_batch on its own context and stream); RCCL (ncclGather over
+// xGMI) brings the 8-byte digests and 1-byte verdicts to the first device, where the
+// de-interleave kernel (framesum_shard.hip) restores global frame order. Frames are
+// independent (eth/crc.go:12-17), so the gather is the only collective.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/framesum.h"
+#include "framesum_internal.h"
+#include "framesum_plan.h"
+
+struct fs_group {
+    int n = 0;
+    std::vector<int> dev;
+    std::vector<fs_ctx*> ctx;
+    std::vector<ncclComm_t> comm;
+    std::vector<hipStream_t> stream;
+    std::vector<uint8_t*> send;  // per device k >= 1: its slab; device 0 sends in place from recv
+    uint8_t* recv = nullptr;     // first device: n slabs back to back
+    uint64_t cap_slab = 0;       // bytes per slab currently allocated
+    std::string err;
+};
+
+namespace {
+
+thread_local std::string g_group_create_err;
+
+fs_status gset(fs_group* g, fs_status code, const std::string& msg) {
+    if (g) g->err = msg;
+    else g_group_create_err = msg;
+    return code;
+}
+
+void free_slabs(fs_group* g) {
+    for (int k = 0; k < g->n; ++k) {
+        if (k > 0 && g->send[k]) {
+            (void)hipSetDevice(g->dev[k]);
+            (void)hipFree(g->send[k]);
+        }
+        g->send[k] = nullptr;
+    }
+    if (g->recv) {
+        (void)hipSetDevice(g->dev[0]);
+        (void)hipFree(g->recv);
+    }
+    g->recv = nullptr;
+    g->cap_slab = 0;
+}
+
+fs_status ensure_slabs(fs_group* g, uint64_t sb) {
+    if (sb <= g->cap_slab) return FS_SUCCESS;
+    for (int k = 0; k < g->n; ++k) {
+        (void)hipSetDevice(g->dev[k]);
+        (void)hipStreamSynchronize(g->stream[k]);
+    }
+    free_slabs(g);
+    if (hipSetDevice(g->dev[0]) != hipSuccess || hipMalloc(&g->recv, sb * (uint64_t)g->n) != hipSuccess)
+        return gset(g, FS_E_NOMEM, "fs_digest_batch_sharded: hipMalloc of the gather buffer failed");
+    g->send[0] = g->recv;
+    for (int k = 1; k < g->n; ++k)
+        if (hipSetDevice(g->dev[k]) != hipSuccess || hipMalloc(&g->send[k], sb) != hipSuccess)
+            return gset(g, FS_E_NOMEM, "fs_digest_batch_sharded: hipMalloc of a shard slab failed");
+    g->cap_slab = sb;
+    return FS_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t fs_shard_count(uint64_t n, uint32_t nshards, uint32_t shard) {
+    return nshards == 0 ? 0 : framesum::plan::shard_count(n, nshards, shard);
+}
+
+uint64_t fs_shard_slab_bytes(uint64_t n, uint32_t nshards) {
+    return nshards == 0 ? 0 : framesum::plan::slab_bytes(framesum::plan::shard_rows(n, nshards));
+}
+
+fs_status fs_group_create(const int* devices, int ndev, fs_group** out) {
+    if (!out) return gset(nullptr, FS_E_INVALID, "fs_group_create: out is NULL");
+    *out = nullptr;
+    if (!devices || ndev <= 0) return gset(nullptr, FS_E_INVALID, "fs_group_create: no devices");
+    for (int k = 0; k < ndev; ++k)
+        for (int j = 0; j < k; ++j)
+            if (devices[j] == devices[k]) return gset(nullptr, FS_E_INVALID, "fs_group_create: a device appears twice");
+    fs_group* g = new (std::nothrow) fs_group();
+    if (!g) return gset(nullptr, FS_E_NOMEM, "fs_group_create: out of host memory");
+    try {
+        g->n = ndev;
+        g->dev.assign(devices, devices + ndev);
+        g->ctx.assign(ndev, nullptr);
+        g->comm.assign(ndev, nullptr);
+        g->stream.assign(ndev, nullptr);
+        g->send.assign(ndev, nullptr);
+    } catch (const std::bad_alloc&) {
+        delete g;
+        return gset(nullptr, FS_E_NOMEM, "fs_group_create: out of host memory");
+    }
+    for (int k = 0; k < ndev; ++k) {
+        const fs_status st = fs_ctx_create(devices[k], &g->ctx[k]);
+        if (st != FS_SUCCESS) {
+            const std::string msg = std::string("fs_group_create: ") + fs_last_error(nullptr);
+            fs_group_destroy(g);
+            return gset(nullptr, st, msg);
+        }
+        hipError_t e = hipSetDevice(devices[k]);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->stream[k], hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            const std::string msg = std::string("fs_group_create: stream: ") + hipGetErrorString(e);
+            fs_group_destroy(g);
+            return gset(nullptr, FS_E_HIP, msg);
+        }
+    }
+    const ncclResult_t r = ncclCommInitAll(g->comm.data(), ndev, devices);
+    if (r != ncclSuccess) {
+        for (auto& c : g->comm) c = nullptr;  // not created
+        const std::string msg = std::string("fs_group_create: ncclCommInitAll: ") + ncclGetErrorString(r);
+        fs_group_destroy(g);
+        return gset(nullptr, FS_E_HIP, msg);
+    }
+    *out = g;
+    return FS_SUCCESS;
+}
+
+fs_status fs_group_destroy(fs_group* g) {
+    if (!g) return FS_E_INVALID;
+    for (int k = 0; k < g->n; ++k) {
+        if (g->stream[k]) {
+            (void)hipSetDevice(g->dev[k]);
+            (void)hipStreamSynchronize(g->stream[k]);
+        }
+    }
+    free_slabs(g);
+    for (int k = 0; k < g->n; ++k) {
+        if (g->comm[k]) (void)ncclCommDestroy(g->comm[k]);
+        if (g->stream[k]) {
+            (void)hipSetDevice(g->dev[k]);
+            (void)hipStreamDestroy(g->stream[k]);
+        }
+        if (g->ctx[k]) fs_ctx_destroy(g->ctx[k]);
+    }
+    delete g;
+    return FS_SUCCESS;
+}
+
+const char* fs_group_last_error(const fs_group* g) { return g ? g->err.c_str() : g_group_create_err.c_str(); }
+
+fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, const uint64_t* const* offsets,
+                                  const uint32_t* const* lengths, uint64_t n, uint32_t mtu, fs_digest* out,
+                                  uint8_t* status) {
+    if (!g) return FS_E_INVALID;
+    g->err.clear();
+    if (n == 0) return FS_SUCCESS;
+    if (!frames || !offsets || !lengths || !out) return gset(g, FS_E_INVALID, "fs_digest_batch_sharded: null pointer");
+    const uint32_t N = (uint32_t)g->n;
+    const uint64_t m = framesum::plan::shard_rows(n, N);
+    if (m > (1ull << 31)) return gset(g, FS_E_INVALID, "fs_digest_batch_sharded: more than 2^31 frames per shard");
+    const uint64_t sb = framesum::plan::slab_bytes(m);
+    fs_status st = ensure_slabs(g, sb);
+    if (st != FS_SUCCESS) return st;
+    // every shard's kernel on its own device and stream, writing its slab (device 0: in place
+    // in the gather buffer)
+    for (uint32_t k = 0; k < N; ++k) {
+        const uint64_t nk = framesum::plan::shard_count(n, N, k);
+        if (nk == 0) continue;
+        if (!frames[k] || !offsets[k] || !lengths[k])
+            return gset(g, FS_E_INVALID, "fs_digest_batch_sharded: null shard pointer");
+        st = fs_digest_batch(g->ctx[k], frames[k], offsets[k], lengths[k], (uint32_t)nk, mtu,
+                             reinterpret_cast<fs_digest*>(g->send[k]), g->send[k] + 8 * m, g->stream[k]);
+        if (st != FS_SUCCESS)
+            return gset(g, st, "fs_digest_batch_sharded: shard " + std::to_string(k) + ": " + fs_last_error(g->ctx[k]));
+    }
+    // the digests + verdicts of every shard to the first device (the only collective)
+    ncclResult_t r = ncclGroupStart();
+    for (uint32_t k = 0; k < N && r == ncclSuccess; ++k)
+        r = ncclGather(g->send[k], k == 0 ? g->recv : nullptr, sb, ncclUint8, 0, g->comm[k], g->stream[k]);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return gset(g, FS_E_HIP, std::string("fs_digest_batch_sharded: ncclGather: ") +
+                                     ncclGetErrorString(r != ncclSuccess ? r : r2));
+    hipError_t e = hipSetDevice(g->dev[0]);
+    if (e == hipSuccess) e = framesum::launch_deinterleave(g->recv, N, n, out, status, g->stream[0]);
+    for (uint32_t k = 0; k < N && e == hipSuccess; ++k) {
+        e = hipSetDevice(g->dev[k]);
+        if (e == hipSuccess) e = hipStreamSynchronize(g->stream[k]);
+    }
+    if (e != hipSuccess) return gset(g, FS_E_HIP, std::string("fs_digest_batch_sharded: ") + hipGetErrorString(e));
+    return FS_SUCCESS;
+}
+
+}  // extern "C"

@@ -50,4 +50,9 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
                          int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force = 0,
                          FsOp op = FsOp::kDigest, uint8_t* wframes = nullptr, uint32_t tx = 0);
 
+// Restore global frame order from nshards gathered round-robin slabs (framesum_plan.h layout):
+// out[i] = slab[i % nshards].digest[i / nshards], status likewise (nullable). framesum_shard.hip.
+hipError_t launch_deinterleave(const uint8_t* gathered, uint32_t nshards, uint64_t n, void* out, uint8_t* status,
+                               hipStream_t stream);
+
 }  // namespace framesum

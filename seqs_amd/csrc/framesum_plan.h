@@ -1,0 +1,135 @@
+// Host-side planning for the framesum entry points, free of HIP so that it compiles on its
+// own: the chunks of a host-staged batch (fs_digest_batch_host), the byte-balanced blocks of
+// fs_digest_batch_multi, and the round-robin shard maps of fs_digest_batch_sharded and its
+// de-interleave kernel. The library includes it; tests/csrc/test_plan.cpp builds it alone
+// under ASan + UBSan (sanitizers on the host code) and checks every invariant
+// on random, out-of-order, overlapping and edge-case batches.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <numeric>
+#include <vector>
+
+namespace framesum {
+namespace plan {
+
+// ---------------------------------------------------------------------------------------
+// Round-robin shards (eth/crc.go:12-17: CRC791 is per call, so frames are
+// independent). Global frame i lives on shard i % N at local index i / N. Shards are padded
+// to m = ceil(n / N) rows for the fixed-size RCCL gather; shard k's gathered slab holds its
+// m 8-byte digests and then its m verdict bytes, 256-byte aligned.
+constexpr uint64_t shard_count(uint64_t n, uint32_t nshards, uint32_t shard) {
+    return shard < n ? (n - shard + nshards - 1) / nshards : 0;
+}
+constexpr uint64_t shard_rows(uint64_t n, uint32_t nshards) { return (n + nshards - 1) / nshards; }
+constexpr uint64_t slab_bytes(uint64_t m) { return (9 * m + 255) / 256 * 256; }
+// byte offsets, in the gathered buffer of nshards slabs, of global frame i's digest and verdict
+constexpr uint64_t gathered_digest_at(uint64_t i, uint32_t nshards, uint64_t m) {
+    return (i % nshards) * slab_bytes(m) + 8 * (i / nshards);
+}
+constexpr uint64_t gathered_status_at(uint64_t i, uint32_t nshards, uint64_t m) {
+    return (i % nshards) * slab_bytes(m) + 8 * m + i / nshards;
+}
+
+// ---------------------------------------------------------------------------------------
+// Host-staged chunks.
+
+// Index of the first frame that does not lie inside [0, frames_bytes) (overflow-safe), or n.
+inline uint32_t first_frame_out_of_range(const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                                         uint64_t frames_bytes, uint32_t extra = 0) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t need = (uint64_t)lengths[i] + extra;
+        if (offsets[i] > frames_bytes || need > frames_bytes - offsets[i]) return i;
+    }
+    return n;
+}
+
+struct Chunk {
+    uint32_t c0, c1;          // frames [c0, c1)
+    uint64_t cpy_lo, cpy_hi;  // host bytes [cpy_lo, cpy_hi) staged for them
+};
+
+// The bytes a staged chunk copies for frames spanning [lo, hi): a 16-B aligned start with a
+// 16-B prefix (frames under 4 bytes are read from up to 12 bytes before their start), and the
+// end rounded up to the dword the engine may read, capped at the buffer.
+inline void copy_span(uint64_t lo, uint64_t hi, uint64_t frames_bytes, uint64_t& cpy_lo, uint64_t& cpy_hi) {
+    cpy_lo = (lo >= 16 ? lo - 16 : 0) & ~uint64_t(15);
+    cpy_hi = (hi + 3) & ~uint64_t(3);
+    if (cpy_hi > frames_bytes) cpy_hi = frames_bytes;
+    if (cpy_hi < cpy_lo) cpy_hi = cpy_lo;
+}
+
+// Cut frames [0, n) into chunks of at most chunk_frames frames whose byte span stays within
+// chunk_bytes (a single frame may exceed it). When a chunk would hold fewer than 64 frames
+// because the next frame lies far away (frames not stored in index order), the chunk takes
+// the rest of the batch instead of a launch per handful of frames. Every frame must already
+// lie inside the buffer (first_frame_out_of_range).
+inline void host_chunks(const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint64_t frames_bytes,
+                        uint64_t chunk_bytes, uint32_t chunk_frames, std::vector<Chunk>& out) {
+    out.clear();
+    uint32_t c0 = 0;
+    while (c0 < n) {
+        uint64_t lo = offsets[c0], hi = offsets[c0] + lengths[c0];
+        uint32_t c1 = c0 + 1;
+        while (c1 < n && c1 - c0 < chunk_frames) {
+            const uint64_t o = offsets[c1], e = o + lengths[c1];
+            const uint64_t nlo = o < lo ? o : lo, nhi = e > hi ? e : hi;
+            if (nhi - nlo > chunk_bytes) break;
+            lo = nlo;
+            hi = nhi;
+            ++c1;
+        }
+        if (c1 < n && c1 - c0 < 64 && hi - lo < chunk_bytes / 4) {
+            for (; c1 < n; ++c1) {
+                const uint64_t o = offsets[c1], e = o + lengths[c1];
+                lo = o < lo ? o : lo;
+                hi = e > hi ? e : hi;
+            }
+        }
+        Chunk c{c0, c1, 0, 0};
+        copy_span(lo, hi, frames_bytes, c.cpy_lo, c.cpy_hi);
+        out.push_back(c);
+        c0 = c1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// fs_digest_batch_multi blocks: nctx blocks of about equal byte counts. The blocks are
+// contiguous runs of the frames in buffer order, so that each context copies only its own
+// bytes: `order` is empty when the offsets are already non-decreasing (block k = frames
+// [cut[k], cut[k+1])), otherwise it lists the frame indices sorted by offset (stable) and
+// block k = order[cut[k] .. cut[k+1]).
+struct MultiPlan {
+    std::vector<uint32_t> order;
+    std::vector<uint32_t> cut;  // nctx + 1 positions, cut[0] = 0, cut[nctx] = n
+    uint32_t frame(uint32_t pos) const { return order.empty() ? pos : order[pos]; }
+};
+
+inline void multi_blocks(const uint64_t* offsets, const uint32_t* lengths, uint32_t n, int nctx, MultiPlan& p) {
+    p.order.clear();
+    p.cut.assign((size_t)nctx + 1, n);
+    p.cut[0] = 0;
+    bool sorted = true;
+    for (uint32_t i = 1; i < n && sorted; ++i) sorted = offsets[i] >= offsets[i - 1];
+    if (!sorted) {
+        p.order.resize(n);
+        std::iota(p.order.begin(), p.order.end(), 0u);
+        std::stable_sort(p.order.begin(), p.order.end(),
+                         [offsets](uint32_t a, uint32_t b) { return offsets[a] < offsets[b]; });
+    }
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += lengths[i];
+    // block k starts at the first position whose running byte count reaches k/nctx of the total
+    uint64_t run = 0;
+    int k = 1;
+    for (uint32_t pos = 0; pos < n && k < nctx; ++pos) {
+        while (k < nctx && (unsigned __int128)run * (unsigned)nctx >= (unsigned __int128)total * (unsigned)k)
+            p.cut[k++] = pos;
+        run += lengths[p.frame(pos)];
+    }
+}
+
+}  // namespace plan
+}  // namespace framesum

@@ -69,6 +69,13 @@ EXPORTED_SYMBOLS = (
     "fs_ctx_set_kernel",
     "fs_host_alloc",
     "fs_host_free",
+    "fs_group_create",
+    "fs_group_destroy",
+    "fs_group_last_error",
+    "fs_shard_count",
+    "fs_shard_slab_bytes",
+    "fs_digest_batch_sharded",
+    "fs_deinterleave",
 )
 
 DIGEST_DTYPE = np.dtype([("crc32", "<u4"), ("ip_csum", "<u2"), ("l4_csum", "<u2")])
@@ -122,6 +129,21 @@ def load_library() -> ctypes.CDLL:
     lib.fs_host_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
     lib.fs_host_free.restype = i32
     lib.fs_host_free.argtypes = [vp, vp]
+    lib.fs_group_create.restype = i32
+    lib.fs_group_create.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(vp)]
+    lib.fs_group_destroy.restype = i32
+    lib.fs_group_destroy.argtypes = [vp]
+    lib.fs_group_last_error.restype = ctypes.c_char_p
+    lib.fs_group_last_error.argtypes = [vp]
+    lib.fs_shard_count.restype = u64
+    lib.fs_shard_count.argtypes = [u64, u32, u32]
+    lib.fs_shard_slab_bytes.restype = u64
+    lib.fs_shard_slab_bytes.argtypes = [u64, u32]
+    lib.fs_digest_batch_sharded.restype = i32
+    lib.fs_digest_batch_sharded.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), u64, u32,
+                                            vp, vp]
+    lib.fs_deinterleave.restype = i32
+    lib.fs_deinterleave.argtypes = [vp, vp, u32, u64, vp, vp, vp]
     _lib = lib
     return lib
 
@@ -255,6 +277,26 @@ class Engine:
         self._check(st, "fs_digest_batch_fcs")
         return out, status
 
+    def deinterleave_device(self, gathered, nshards: int, n: int, out=None, status=None, stream=None):
+        """Global frame order from nshards gathered round-robin slabs (fs_deinterleave):
+        `gathered` is a uint8 CUDA tensor of nshards * shard_slab_bytes(n, nshards) bytes, slab k =
+        shard k's digests then its verdicts. Returns (out (n, 2) int32, status (n,) uint8)."""
+        import torch
+
+        assert gathered.is_cuda and gathered.dtype == torch.uint8 and gathered.is_contiguous()
+        assert gathered.numel() >= nshards * shard_slab_bytes(n, nshards)
+        if out is None:
+            out = torch.empty((n, 2), dtype=torch.int32, device=gathered.device)
+        if status is None:
+            status = torch.empty((n,), dtype=torch.uint8, device=gathered.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(gathered.device)
+        st = self.lib.fs_deinterleave(self._ctx, ctypes.c_void_p(gathered.data_ptr()), nshards, n,
+                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()),
+                                      ctypes.c_void_p(stream.cuda_stream))
+        self._check(st, "fs_deinterleave")
+        return out, status
+
     # ---- host-staged path (numpy in, numpy out) -----------------------------
     def host_empty(self, shape, dtype=np.uint8) -> np.ndarray:
         """A numpy array in pinned host memory (fs_host_alloc), freed with the array."""
@@ -287,11 +329,13 @@ class Engine:
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
         n = int(lengths.size)
+        assert offsets.size == n, "offsets and lengths must describe the same frames"
         if out is None:
             out = np.zeros(n, dtype=DIGEST_DTYPE)
         if status is None:
             status = np.zeros(n, dtype=np.uint8)
         assert out.dtype == DIGEST_DTYPE and out.size >= n and status.dtype == np.uint8 and status.size >= n
+        assert out.flags["C_CONTIGUOUS"] and status.flags["C_CONTIGUOUS"], "out / status are written in place"
         if n == 0:
             return out, status
         st = self.lib.fs_digest_batch_host(
@@ -317,6 +361,7 @@ class Engine:
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
         n = int(lengths.size)
+        assert offsets.size == n, "offsets and lengths must describe the same frames"
         out = np.zeros(n, dtype=DIGEST_DTYPE)
         status = np.zeros(n, dtype=np.uint8)
         if n == 0:
@@ -373,9 +418,76 @@ def digest_host_multi(engines: Sequence["Engine"], frames: np.ndarray, offsets: 
                                    offsets.ctypes.data_as(ctypes.c_void_p), lengths.ctypes.data_as(ctypes.c_void_p),
                                    n, mtu, out.ctypes.data_as(ctypes.c_void_p), status.ctypes.data_as(ctypes.c_void_p))
     if st != FS_SUCCESS:
-        msgs = "; ".join(f"ctx {k}: {e.lib.fs_last_error(e._ctx).decode()}" for k, e in enumerate(engines))
+        # every entry point clears its context's message first: only failing contexts hold one
+        msgs = "; ".join(f"ctx {k}: {m}" for k, e in enumerate(engines)
+                         if (m := e.lib.fs_last_error(e._ctx).decode()))
         raise FramesumError(f"fs_digest_batch_multi failed ({st}): {msgs}")
     return out, status
+
+def shard_count(n: int, nshards: int, shard: int) -> int:
+    """Frames of shard `shard` when n global frames go round-robin over nshards shards (C ABI)."""
+    return int(load_library().fs_shard_count(n, nshards, shard))
+
+
+def shard_slab_bytes(n: int, nshards: int) -> int:
+    """Bytes of one shard's gathered slab: ceil(n/N) digests then ceil(n/N) verdicts, 256-B aligned."""
+    return int(load_library().fs_shard_slab_bytes(n, nshards))
+
+
+class Group:
+    """One host process driving several GPUs (fs_group): a context, a stream and an RCCL
+    communicator per device. `digest_sharded` runs fs_digest_batch_sharded: every device digests
+    its round-robin shard, ncclGather brings the digests to the first device, a de-interleave
+    kernel restores global order there."""
+
+    def __init__(self, devices: Sequence[int]):
+        self.lib = load_library()
+        self.devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        g = ctypes.c_void_p()
+        st = self.lib.fs_group_create(arr, len(self.devices), ctypes.byref(g))
+        if st != FS_SUCCESS:
+            raise FramesumError(f"fs_group_create({self.devices}) failed ({st}): "
+                                f"{self.lib.fs_group_last_error(None).decode()}")
+        self._g = g
+
+    def close(self) -> None:
+        if getattr(self, "_g", None):
+            self.lib.fs_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def digest_sharded(self, shards, n: int, mtu: int = 0, out=None, status=None):
+        """shards[k] = (frames, offsets int64, lengths int32) CUDA tensors on devices[k] holding
+        shard k (fs_shard_count(n, N, k) frames). Returns (out (n, 2) int32, status (n,) uint8)
+        on devices[0], in global frame order (synchronous)."""
+        import torch
+
+        N = len(self.devices)
+        assert len(shards) == N
+        vp = ctypes.c_void_p
+        fr, of, ln = (vp * N)(), (vp * N)(), (vp * N)()
+        for k, (f, o, l) in enumerate(shards):
+            assert f.dtype == torch.uint8 and o.dtype == torch.int64 and l.dtype == torch.int32
+            assert f.is_contiguous() and o.is_contiguous() and l.is_contiguous()
+            assert l.numel() == shard_count(n, N, k) and o.numel() == l.numel()
+            assert f.device.index == self.devices[k]
+            fr[k], of[k], ln[k] = f.data_ptr(), o.data_ptr(), l.data_ptr()
+        dev = torch.device("cuda", self.devices[0])
+        if out is None:
+            out = torch.empty((n, 2), dtype=torch.int32, device=dev)
+        if status is None:
+            status = torch.empty((n,), dtype=torch.uint8, device=dev)
+        st = self.lib.fs_digest_batch_sharded(self._g, fr, of, ln, n, mtu, vp(out.data_ptr()), vp(status.data_ptr()))
+        if st != FS_SUCCESS:
+            raise FramesumError(f"fs_digest_batch_sharded failed ({st}): {self.lib.fs_group_last_error(self._g).decode()}")
+        return out, status
+
 
 def pack_frames(frames: Sequence[bytes], align: int = 4):
     """Pack a list of frames into one buffer (each frame at an `align`-aligned offset)."""

@@ -97,6 +97,11 @@ class ShardedDigest:
         self.digest_fn = digest_fn
 
     def __call__(self, frames, offsets, lengths, n_global: int, mtu: int = 0):
+        import torch.distributed as dist
+
         words, status = self.digest_fn(frames, offsets, lengths, mtu)
+        if words.is_cuda and dist.get_backend(self.group) == "gloo":
+            # gloo gathers host tensors: the engine's device results travel as CPU copies
+            words, status = words.cpu(), status.cpu()
         _, finish = gather_digests(words, status, self.world, self.rank, n_global, self.group)
         return finish()

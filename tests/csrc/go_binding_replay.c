@@ -1,0 +1,140 @@
+/* A C replay of go/eth/digest_gpu.go (the cgo binding a seqs maintainer adds) through the
+ * framesum C ABI: the same packing of a [][]byte batch -- each frame at a 4-byte aligned
+ * offset, 4 spare bytes per frame for FillBatch with appendFCS, 16 spare bytes after the last
+ * frame, all in pinned memory from fs_host_alloc grown on demand -- and the same calls:
+ *   digest  GPU.DigestBatch   -> fs_digest_batch_host
+ *   fill    GPU.FillBatch     -> fs_fill_batch_host, then the filled bytes copied back out
+ *   multi   GPUs.DigestBatch  -> fs_digest_batch_multi over nctx contexts (all on device 0 here)
+ * Input: a frame list file (u32 n, then n x {u32 len, len bytes}). Output: n fs_digest, n
+ * verdict bytes, and for fill the filled frames as a frame list (len + 4 bytes with FCS).
+ * tests/test_go_binding.py compares everything with the CPU oracle.
+ * usage: go_binding_replay digest|fill|fill_fcs|multi <in.lst> <mtu> <out.bin> [nctx] */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "framesum.h"
+
+typedef struct {
+    uint32_t n;
+    uint32_t* len;
+    uint8_t** data;
+} frame_list;
+
+static int read_list(const char* path, frame_list* fl) {
+    FILE* f = fopen(path, "rb");
+    if (!f || fread(&fl->n, 4, 1, f) != 1) return -1;
+    fl->len = calloc(fl->n + 1, 4);
+    fl->data = calloc(fl->n + 1, sizeof(uint8_t*));
+    for (uint32_t i = 0; i < fl->n; ++i) {
+        if (fread(&fl->len[i], 4, 1, f) != 1) return -1;
+        fl->data[i] = malloc(fl->len[i] + 4); /* Go: cap >= len + 4 for appendFCS */
+        if (fl->len[i] && fread(fl->data[i], 1, fl->len[i], f) != fl->len[i]) return -1;
+    }
+    fclose(f);
+    return 0;
+}
+
+/* GPU.stage: pack into grow-on-demand pinned memory */
+typedef struct {
+    fs_ctx* ctx;
+    uint8_t* pin;
+    uint64_t pcap;
+    uint64_t* offs;
+    uint32_t* lens;
+} gpu;
+
+static uint8_t* stage(gpu* g, const frame_list* fl, uint32_t spare, uint64_t* total_out) {
+    uint64_t total = 0;
+    g->offs = realloc(g->offs, 8 * (size_t)(fl->n + 1));
+    g->lens = realloc(g->lens, 4 * (size_t)(fl->n + 1));
+    for (uint32_t i = 0; i < fl->n; ++i) {
+        g->offs[i] = total;
+        g->lens[i] = fl->len[i];
+        total += ((uint64_t)fl->len[i] + spare + 3) & ~(uint64_t)3;
+    }
+    total += 16;
+    if (total > g->pcap) {
+        if (g->pin) fs_host_free(g->ctx, g->pin);
+        g->pin = NULL;
+        g->pcap = 0;
+        void* p = NULL;
+        if (fs_host_alloc(g->ctx, total, &p) != FS_SUCCESS) return NULL;
+        g->pin = p;
+        g->pcap = total;
+    }
+    for (uint32_t i = 0; i < fl->n; ++i) memcpy(g->pin + g->offs[i], fl->data[i], fl->len[i]);
+    *total_out = total;
+    return g->pin;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 5) {
+        fprintf(stderr, "usage: %s digest|fill|fill_fcs|multi in.lst mtu out.bin [nctx]\n", argv[0]);
+        return 2;
+    }
+    const char* mode = argv[1];
+    const uint32_t mtu = (uint32_t)strtoul(argv[3], NULL, 10);
+    frame_list fl;
+    if (read_list(argv[2], &fl) != 0) {
+        fprintf(stderr, "cannot read %s\n", argv[2]);
+        return 2;
+    }
+    gpu g = {0};
+    if (fs_ctx_create(0, &g.ctx) != FS_SUCCESS) {
+        fprintf(stderr, "fs_ctx_create: %s\n", fs_last_error(NULL));
+        return 1;
+    }
+    fs_digest* out = calloc(fl.n + 1, sizeof(fs_digest));
+    uint8_t* ver = calloc(fl.n + 1, 1);
+    const int fill = !strcmp(mode, "fill") || !strcmp(mode, "fill_fcs");
+    const uint32_t spare = !strcmp(mode, "fill_fcs") ? 4u : 0u;
+    uint64_t total = 0;
+    uint8_t* buf = fl.n ? stage(&g, &fl, spare, &total) : NULL;
+    if (fl.n && !buf) {
+        fprintf(stderr, "fs_host_alloc: %s\n", fs_last_error(g.ctx));
+        return 1;
+    }
+    fs_status st = FS_SUCCESS;
+    if (fl.n && !strcmp(mode, "digest")) {
+        st = fs_digest_batch_host(g.ctx, buf, total, g.offs, g.lens, fl.n, mtu, out, ver);
+    } else if (fl.n && fill) {
+        st = fs_fill_batch_host(g.ctx, buf, total, g.offs, g.lens, fl.n, mtu,
+                                FS_FILL_CSUM | (spare ? FS_FCS_APPEND : 0u), out, ver);
+        for (uint32_t i = 0; st == FS_SUCCESS && i < fl.n; ++i)
+            memcpy(fl.data[i], buf + g.offs[i], fl.len[i] + spare);
+    } else if (fl.n && !strcmp(mode, "multi")) {
+        const int nctx = argc > 5 ? atoi(argv[5]) : 2;
+        fs_ctx** ctxs = calloc((size_t)nctx, sizeof(fs_ctx*));
+        ctxs[0] = g.ctx;
+        for (int k = 1; k < nctx; ++k)
+            if (fs_ctx_create(0, &ctxs[k]) != FS_SUCCESS) {
+                fprintf(stderr, "fs_ctx_create: %s\n", fs_last_error(NULL));
+                return 1;
+            }
+        st = fs_digest_batch_multi(ctxs, nctx, buf, total, g.offs, g.lens, fl.n, mtu, out, ver);
+        for (int k = 1; k < nctx; ++k) fs_ctx_destroy(ctxs[k]);
+        free(ctxs);
+    }
+    if (st != FS_SUCCESS) {
+        fprintf(stderr, "%s failed (%d): %s\n", mode, st, fs_last_error(g.ctx));
+        return 1;
+    }
+    FILE* o = fopen(argv[4], "wb");
+    fwrite(out, sizeof(fs_digest), fl.n, o);
+    fwrite(ver, 1, fl.n, o);
+    if (fill) {
+        fwrite(&fl.n, 4, 1, o);
+        for (uint32_t i = 0; i < fl.n; ++i) {
+            const uint32_t l = fl.len[i] + spare;
+            fwrite(&l, 4, 1, o);
+            fwrite(fl.data[i], 1, l, o);
+        }
+    }
+    fclose(o);
+    if (g.pin) fs_host_free(g.ctx, g.pin);
+    fs_ctx_destroy(g.ctx);
+    printf("%s: %u frames\n", mode, fl.n);
+    return 0;
+}

@@ -1,0 +1,168 @@
+// Host-logic checks of seqs_amd/csrc/framesum_plan.h, built on its own under ASan + UBSan
+// (tests/csrc/Makefile, run by tests/test_host_sanitizers.py): the chunks of the
+// host-staged path, the blocks of fs_digest_batch_multi and the round-robin shard / gather /
+// de-interleave maps, on random batches that are in order, shuffled, sparse, overlapping,
+// empty, zero-length, huge-offset, and with more contexts than frames.
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../../seqs_amd/csrc/framesum_plan.h"
+
+using namespace framesum::plan;
+
+static int g_fail = 0;
+#define CHECK(c)                                                              \
+    do {                                                                      \
+        if (!(c)) {                                                           \
+            std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #c); \
+            if (++g_fail > 20) std::exit(1);                                  \
+        }                                                                     \
+    } while (0)
+
+struct Batch {
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    uint64_t bytes = 0;
+};
+
+static Batch make_batch(std::mt19937_64& rng, uint32_t n, int kind) {
+    Batch b;
+    b.off.resize(n);
+    b.len.resize(n);
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t L = kind == 3 ? 0u : (uint32_t)(rng() % 9100);
+        b.len[i] = L;
+        if (kind == 2 && rng() % 4 == 0) pos += rng() % (64u << 20);  // sparse: big gaps
+        b.off[i] = pos;
+        pos += (L + 3) & ~3u;
+        if (kind == 4 && i > 0 && rng() % 3 == 0) b.off[i] = b.off[rng() % i];  // overlapping / repeated
+    }
+    b.bytes = pos + 16;
+    if (kind == 1) {  // shuffled: offsets not in index order
+        for (uint32_t i = n; i > 1; --i) {
+            const uint32_t j = (uint32_t)(rng() % i);
+            std::swap(b.off[i - 1], b.off[j]);
+            std::swap(b.len[i - 1], b.len[j]);
+        }
+    }
+    return b;
+}
+
+static void check_chunks(const Batch& b, uint64_t chunk_bytes, uint32_t chunk_frames) {
+    const uint32_t n = (uint32_t)b.len.size();
+    CHECK(first_frame_out_of_range(b.off.data(), b.len.data(), n, b.bytes) == n);
+    std::vector<Chunk> ch;
+    host_chunks(b.off.data(), b.len.data(), n, b.bytes, chunk_bytes, chunk_frames, ch);
+    uint32_t next = 0;
+    for (const Chunk& c : ch) {
+        CHECK(c.c0 == next && c.c1 > c.c0 && c.c1 <= n);
+        CHECK(c.cpy_lo % 16 == 0 && c.cpy_lo <= c.cpy_hi && c.cpy_hi <= b.bytes);
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (uint32_t i = c.c0; i < c.c1; ++i) {
+            // every byte the engine may touch for frame i lies in the staged copy: 12 B before
+            // its start (or the buffer start) up to its dword-rounded end (or the buffer end)
+            const uint64_t s = b.off[i], e = s + b.len[i];
+            CHECK(c.cpy_lo <= (s >= 12 ? s - 12 : 0));
+            CHECK(std::min<uint64_t>((e + 3) & ~uint64_t(3), b.bytes) <= c.cpy_hi);
+            lo = std::min(lo, s);
+            hi = std::max(hi, e);
+        }
+        const bool single = c.c1 - c.c0 == 1, rest = c.c1 == n;
+        CHECK(single || rest || hi - lo <= chunk_bytes);
+        CHECK(c.c1 - c.c0 <= chunk_frames || rest);
+        next = c.c1;
+    }
+    CHECK(next == n);
+}
+
+static void check_multi(const Batch& b, int nctx) {
+    const uint32_t n = (uint32_t)b.len.size();
+    MultiPlan p;
+    multi_blocks(b.off.data(), b.len.data(), n, nctx, p);
+    CHECK((int)p.cut.size() == nctx + 1 && p.cut[0] == 0 && p.cut[nctx] == n);
+    for (int k = 0; k < nctx; ++k) CHECK(p.cut[k] <= p.cut[k + 1]);
+    std::vector<uint8_t> seen(n, 0);
+    uint64_t total = 0, maxlen = 0;
+    for (uint32_t pos = 0; pos < n; ++pos) {
+        const uint32_t f = p.frame(pos);
+        CHECK(f < n);
+        if (f < n) seen[f]++;
+        if (pos > 0) CHECK(b.off[p.frame(pos - 1)] <= b.off[f]);  // buffer order inside every block
+        total += b.len[f];
+        maxlen = std::max<uint64_t>(maxlen, b.len[f]);
+    }
+    for (uint32_t i = 0; i < n; ++i) CHECK(seen[i] == 1);  // a permutation
+    for (int k = 0; k < nctx; ++k) {
+        uint64_t bytes = 0;
+        for (uint32_t pos = p.cut[k]; pos < p.cut[k + 1]; ++pos) bytes += b.len[p.frame(pos)];
+        CHECK(bytes * (uint64_t)nctx <= total + (uint64_t)nctx * maxlen);  // byte balance
+    }
+}
+
+static void check_shards(uint64_t n, uint32_t N) {
+    uint64_t sum = 0;
+    for (uint32_t k = 0; k < N; ++k) sum += shard_count(n, N, k);
+    CHECK(sum == n);
+    const uint64_t m = shard_rows(n, N), sb = slab_bytes(m);
+    CHECK(sb % 256 == 0 && sb >= 9 * m);
+    // simulate: shard k writes local frame j's digest = global index (j*N + k); the gather puts
+    // slab k at k*sb; the de-interleave map must give back global order
+    std::vector<uint64_t> gathered((N * sb) / 8 + 1, ~0ull);
+    std::vector<uint8_t> gst(N * sb, 0xEE);
+    for (uint32_t k = 0; k < N; ++k)
+        for (uint64_t j = 0; j < shard_count(n, N, k); ++j) {
+            const uint64_t at = k * sb + 8 * j;
+            CHECK(at % 8 == 0 && at + 8 <= N * sb);
+            gathered[at / 8] = j * N + k;
+            const uint64_t sat = k * sb + 8 * m + j;
+            CHECK(sat < N * sb && sat >= k * sb + 8 * m);
+            gst[sat] = (uint8_t)((j * N + k) & 0x7F);
+        }
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t at = gathered_digest_at(i, N, m), sat = gathered_status_at(i, N, m);
+        CHECK(at % 8 == 0 && at + 8 <= N * sb && sat < N * sb);
+        CHECK(gathered[at / 8] == i);
+        CHECK(gst[sat] == (uint8_t)(i & 0x7F));
+    }
+}
+
+int main() {
+    std::mt19937_64 rng(12345);
+    // chunks: every batch kind, several chunk sizes (small ones force many chunks)
+    for (int kind = 0; kind < 5; ++kind)
+        for (uint32_t n : {0u, 1u, 2u, 7u, 63u, 64u, 65u, 1000u, 5000u})
+            for (uint64_t cb : {uint64_t(4096), uint64_t(65536), uint64_t(16) << 20}) {
+                const Batch b = make_batch(rng, n, kind);
+                check_chunks(b, cb, kind == 0 ? 100u : (1u << 20));
+            }
+    // out-of-range detection, including offsets whose end would overflow 64 bits
+    {
+        std::vector<uint64_t> off = {0, 100, UINT64_MAX - 2, 50};
+        std::vector<uint32_t> len = {10, 20, 10, 10};
+        CHECK(first_frame_out_of_range(off.data(), len.data(), 4, 1000) == 2);
+        CHECK(first_frame_out_of_range(off.data(), len.data(), 2, 1000) == 2);
+        CHECK(first_frame_out_of_range(off.data(), len.data(), 2, 120) == 2);
+        CHECK(first_frame_out_of_range(off.data(), len.data(), 2, 119) == 1);
+        CHECK(first_frame_out_of_range(off.data(), len.data(), 1, 13, 4) == 0);
+        CHECK(first_frame_out_of_range(off.data(), len.data(), 1, 14, 4) == 1);
+    }
+    // multi blocks: more contexts than frames, empty batches, unordered and overlapping batches
+    for (int kind = 0; kind < 5; ++kind)
+        for (uint32_t n : {0u, 1u, 3u, 8u, 9u, 100u, 4097u})
+            for (int nctx : {1, 2, 3, 8, 16})
+                check_multi(make_batch(rng, n, kind), nctx);
+    // shard maps for the group entry and the bench's gather
+    for (uint32_t N : {1u, 2u, 3u, 4u, 8u})
+        for (uint64_t n : {uint64_t(0), uint64_t(1), uint64_t(2), uint64_t(7), uint64_t(8), uint64_t(9),
+                           uint64_t(1000), uint64_t(65537), uint64_t(1) << 20})
+            check_shards(n, N);
+    if (g_fail) {
+        std::fprintf(stderr, "%d check(s) failed\n", g_fail);
+        return 1;
+    }
+    std::printf("plan checks OK\n");
+    return 0;
+}
