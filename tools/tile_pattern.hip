@@ -1,0 +1,165 @@
+// Access-pattern microbenchmark for the digest kernel's decomposition (measurement tool, no
+// CRC compute): persistent waves stream tiles of 64/G consecutive 1500-B frames (packed back
+// to back, as the C2/C4 batches), G lanes per frame, rows of 16*G bytes, a ring of PF row
+// loads per wave that runs on across tiles (no drain at tile ends). Rows either aligned to
+// their size in memory (AL = 1: full 128-B lines for G >= 8; the partial head and tail rows'
+// lanes outside the frame issue no load) or anchored at the frame end (AL = 0, the current
+// kernel's rows for G = 4). Compared with a plain grid-stride stream, on a 98.3 MB C2 batch
+// (one launch) and a 1.57 GB C4 batch (steady state), on 1 and 4 streams.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+#define CHECK(x)                                                                          \
+    do {                                                                                  \
+        hipError_t e = (x);                                                               \
+        if (e != hipSuccess) {                                                            \
+            printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__);                     \
+            exit(1);                                                                      \
+        }                                                                                 \
+    } while (0)
+
+template <int G, int PF, bool AL, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
+                                                    uint32_t* out) {
+    constexpr int FPT = 64 / G;
+    constexpr uint32_t RB = 16u * G;
+    const uint32_t lane = threadIdx.x & 63u, grp = lane / G, gl = lane % G;
+    const uint32_t gwave = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;  // wave-major
+    const uint32_t nwaves = gridDim.x * WPB;
+    const uint32_t ntiles = (nframes + FPT - 1) / FPT;
+    const uint32_t my_tiles = gwave < ntiles ? (ntiles - gwave + nwaves - 1) / nwaves : 0;
+    const int Rmax = AL ? (int)((flen + RB - 1) / RB + 1) : (int)((flen + RB - 1) / RB);
+    const int nq = (int)my_tiles * Rmax;
+    // address of flattened row q for this lane; false if the lane loads nothing
+    auto addr = [&](int q, const u32x4_a4*& p) -> bool {
+        const int k = q / Rmax, r = q - k * Rmax;
+        const uint32_t f = (gwave + (uint32_t)k * nwaves) * FPT + grp;
+        if (f >= nframes) return false;
+        const uint64_t S = (uint64_t)f * flen, E = S + flen;
+        uint64_t a;
+        if (AL) {
+            const uint64_t b0 = S / RB, b1 = (E - 1) / RB;
+            if (b0 + (uint64_t)r > b1) return false;
+            a = (b0 + r) * RB + 16u * gl;
+            if (a + 16 <= S || a >= E) return false;
+        } else {
+            const uint64_t E4 = (E + 3) & ~uint64_t(3);
+            const int64_t s = (int64_t)E4 - (int64_t)RB * (Rmax - r) + 16 * (int64_t)gl;
+            if (s + 16 <= (int64_t)S) return false;
+            a = (uint64_t)(s < (int64_t)S ? (int64_t)(S & ~uint64_t(3)) : s);
+        }
+        p = reinterpret_cast<const u32x4_a4*>(base + a);
+        return true;
+    };
+    uint32_t acc = 0;
+    u32x4 pf[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        const u32x4_a4* p;
+        pf[i] = (i < nq && addr(i, p)) ? *p : u32x4{0, 0, 0, 0};
+    }
+    for (int q0 = 0; q0 < nq; q0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            acc = (acc * 3u) ^ pf[i].x ^ pf[i].y ^ pf[i].z ^ pf[i].w;
+            const int qn = q0 + i + PF;
+            const u32x4_a4* p;
+            if (qn < nq && addr(qn, p)) pf[i] = *p;
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int PF, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_stream(const u32x4* __restrict__ p, size_t n16, uint32_t* out) {
+    uint32_t acc = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (PF - 1) * stride < n16; i += PF * stride) {
+        u32x4 v[PF];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) v[k] = p[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) acc = (acc * 3u) ^ v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    for (; i < n16; i += stride) {
+        const u32x4 a = p[i];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+int main(int argc, char** argv) {
+    const uint32_t flen = 1500;
+    const bool big = argc > 1 && std::string(argv[1]) == "c4";
+    const uint32_t nf = big ? (1u << 20) : 65536u;
+    const size_t nbytes = (size_t)nf * flen;
+    const int NB = big ? 2 : 6;
+    std::vector<uint8_t*> bufs(NB);
+    for (auto& b : bufs) {
+        CHECK(hipMalloc(&b, nbytes + 4096));
+        CHECK(hipMemset(b, 0x5a, nbytes + 4096));
+    }
+    uint32_t* out;
+    CHECK(hipMalloc(&out, 64));
+    hipDeviceProp_t prop;
+    CHECK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    hipStream_t st[4];
+    for (auto& x : st) CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    printf("batch %u x %u B = %zu bytes, %d rotated, %d CUs\n", nf, flen, nbytes, NB, cus);
+    const int reps = big ? 40 : 400;
+    auto run = [&](auto launch, const char* name) {
+        double res[2];
+        int k = 0;
+        for (int ns : {1, 4}) {
+            for (int pass = 0; pass < 2; ++pass) {
+                CHECK(hipDeviceSynchronize());
+                auto t0 = std::chrono::steady_clock::now();
+                for (int i = 0; i < reps; ++i) launch(i, st[i % ns]);
+                CHECK(hipDeviceSynchronize());
+                res[k] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+            }
+            ++k;
+        }
+        printf("%-44s 1 stream %9.2f us %7.0f GB/s | 4 streams %9.2f us %7.0f GB/s\n", name, res[0],
+               nbytes / (res[0] * 1e-6) / 1e9, res[1], nbytes / (res[1] * 1e-6) / 1e9);
+    };
+#define TILES(G, PF, AL, WPB)                                                                              \
+    run([&](int i, hipStream_t s) {                                                                       \
+        hipLaunchKernelGGL((k_tiles<G, PF, AL, WPB>), dim3(cus), dim3(64 * WPB), 0, s, bufs[i % NB], nf, flen, out); \
+    }, "tiles G=" #G " PF=" #PF " AL=" #AL " waves/CU=" #WPB)
+#define STREAM(PF, WPB, GRIDMUL)                                                                          \
+    run([&](int i, hipStream_t s) {                                                                       \
+        hipLaunchKernelGGL((k_stream<PF, WPB>), dim3(cus * GRIDMUL), dim3(64 * WPB), 0, s,                \
+                           (const u32x4*)bufs[i % NB], nbytes / 16, out);                                 \
+    }, "stream PF=" #PF " waves/WG=" #WPB " WG/CU=" #GRIDMUL)
+    STREAM(4, 4, 2);
+    STREAM(6, 16, 1);
+    STREAM(4, 16, 1);
+    TILES(4, 6, false, 16);
+    TILES(4, 6, true, 16);
+    TILES(8, 6, true, 16);
+    TILES(8, 4, true, 16);
+    TILES(8, 8, true, 16);
+    TILES(16, 4, true, 16);
+    TILES(16, 6, true, 16);
+    TILES(16, 6, false, 16);
+    TILES(32, 4, true, 16);
+    TILES(64, 4, true, 16);
+    TILES(64, 6, true, 16);
+    TILES(64, 4, false, 16);
+    TILES(8, 6, true, 8);
+    TILES(16, 8, true, 8);
+    TILES(4, 6, false, 16);
+    STREAM(4, 4, 2);
+    return 0;
+}
