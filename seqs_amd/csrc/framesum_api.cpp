@@ -45,6 +45,7 @@ struct fs_ctx {
     int device = 0;
     int num_cus = 0;
     FsTables* d_tables = nullptr;
+    framesum::FsTablesW* d_tables_w = nullptr;
     // host-mapped word the kernels set when a batch has widely mixed lengths (launch_digest)
     volatile uint32_t* h_report = nullptr;
     uint32_t* d_report = nullptr;
@@ -159,6 +160,14 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
     e = hipMalloc(&ctx->d_tables, sizeof(FsTables));
     if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, h, sizeof(FsTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
+        framesum::FsTablesW* hw = new (std::nothrow) framesum::FsTablesW;
+        if (!hw) e = hipErrorOutOfMemory;
+        if (hw) framesum::build_tables_w(hw);
+        if (e == hipSuccess) e = hipMalloc(&ctx->d_tables_w, sizeof(framesum::FsTablesW));
+        if (e == hipSuccess) e = hipMemcpy(ctx->d_tables_w, hw, sizeof(framesum::FsTablesW), hipMemcpyHostToDevice);
+        delete hw;
+    }
+    if (e == hipSuccess) {
         void* hp = nullptr;
         e = hipHostMalloc(&hp, 64, hipHostMallocMapped);
         if (e == hipSuccess) {
@@ -203,6 +212,7 @@ fs_status fs_ctx_destroy(fs_ctx* ctx) {
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     if (ctx->h_report) (void)hipHostFree(const_cast<uint32_t*>(ctx->h_report));
     (void)hipFree(ctx->d_tables);
+    (void)hipFree(ctx->d_tables_w);
     delete ctx;
     return FS_SUCCESS;
 }
@@ -221,7 +231,7 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
     FS_HIP(ctx, hipSetDevice(ctx->device));
     FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
                                         reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
-                                        ctx->d_report, ctx->force_kernel));
+                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kDigest, nullptr, 0, ctx->d_tables_w));
     return FS_SUCCESS;
 }
 
@@ -238,7 +248,7 @@ fs_status fs_fill_batch(fs_ctx* ctx, uint8_t* frames, const uint64_t* offsets, c
     FS_HIP(ctx, hipSetDevice(ctx->device));
     FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
                                         reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
-                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFill, frames, flags));
+                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFill, frames, flags, ctx->d_tables_w));
     return FS_SUCCESS;
 }
 
@@ -254,7 +264,7 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
     FS_HIP(ctx, hipSetDevice(ctx->device));
     FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
                                         reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
-                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFcs));
+                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFcs, nullptr, 0, ctx->d_tables_w));
     return FS_SUCCESS;
 }
 
@@ -303,7 +313,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
         FS_HIP(ctx, framesum::launch_digest(base, sl.d_offsets, sl.d_lengths, cnt, mtu, ctx->d_tables, sl.d_out,
                                             status ? sl.d_status : nullptr, ks, ctx->num_cus, ctx->h_report,
-                                            ctx->d_report, ctx->force_kernel));
+                                            ctx->d_report, ctx->force_kernel, framesum::FsOp::kDigest, nullptr, 0, ctx->d_tables_w));
         FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
         sl.used = true;
         FS_HIP(ctx, hipMemcpyAsync(h_out + c0, sl.d_out, (size_t)cnt * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
@@ -360,7 +370,7 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
     uint8_t* base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
     FS_HIP(ctx, framesum::launch_digest(base, sl.d_offsets, sl.d_lengths, n, mtu, ctx->d_tables, sl.d_out,
                                         status ? sl.d_status : nullptr, ks, ctx->num_cus, ctx->h_report,
-                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFill, base, flags));
+                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFill, base, flags, ctx->d_tables_w));
     FS_HIP(ctx, hipMemcpyAsync(frames + lo, sl.d_frames + (lo - cpy_lo), hi - lo, hipMemcpyDeviceToHost, ks));
     FS_HIP(ctx, hipMemcpyAsync(h_out, sl.d_out, (size_t)n * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
     if (status) FS_HIP(ctx, hipMemcpyAsync(h_st, sl.d_status, n, hipMemcpyDeviceToHost, ks));
@@ -480,7 +490,7 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
     ctx->err.clear();
-    if (variant < 0 || variant > 2) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0, 1 or 2");
+    if (variant < 0 || variant > 3) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0, 1, 2 or 3");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
 }

@@ -128,9 +128,31 @@ constexpr uint32_t kPlainChunk0 = 65536 / 1024;                     // first 1-K
 constexpr uint32_t kPlainChunks = kLdsRegionA / 1024;               // 40 pieces, to LDS [0, 40 KB)
 constexpr uint32_t kDmaPerWave = (kPlainChunks + kWavesPerBlock - 1) / kWavesPerBlock;
 
-// The workgroup's LDS image (static allocation of digest_kernel). Namespace scope, so the
+// ---- LDS map of the 16-lane kernel (digest_kernel_w, below): the 13 plain tables of FsTablesW,
+// region A (Z_256), 16 x 1-KB header slots (16 frame dwords per frame), 16 x per-wave scratch.
+constexpr uint32_t kW_Z16 = 0, kW_Z32 = 4096, kW_Z48 = 8192, kW_Z64 = 12288, kW_Z128 = 16384, kW_Z192 = 20480;
+constexpr uint32_t kW_Z12 = 24576, kW_Z8 = 28672, kW_Zfin = 32768, kW_Z1024 = 49152;
+constexpr uint32_t kW_RegionA = kTablesWPlainBytes;
+constexpr int kHdrDwW = 16;
+constexpr uint32_t kHdrWaveW = 4u * kHdrDwW * kFramesPerTile;  // 1 KB
+constexpr uint32_t kW_Hdr = kTablesWLdsBytes;
+constexpr uint32_t kW_Wave = kW_Hdr + kWavesPerBlock * kHdrWaveW;
+// per-wave scratch: parked parse (12 dwords x 16 frames, [k >> 2][frame][k & 3]), the passes'
+// {Y, csum} per frame, and two super-tile geometry buffers (the one being consumed, the next)
+constexpr uint32_t kW_Park = 0, kW_Ycs = 768, kW_Geo = 896, kW_GeoBytes = 320;
+constexpr uint32_t kW_GeoOrder = 256, kW_GeoP = 272, kW_GeoH = 288, kW_GeoNpass = 304;
+// the next super-tile's descriptors, by one dword LDS-DMA: 16 offsets (u64), 16 lengths (u32)
+constexpr uint32_t kW_Desc = kW_Geo + 2 * kW_GeoBytes, kW_DescLen = 128;
+constexpr uint32_t kW_WaveBytes = kW_Desc + 256;
+constexpr uint32_t kW_LdsBytes = kW_Wave + kWavesPerBlock * kW_WaveBytes;
+static_assert(kW_LdsBytes <= 160 * 1024, "LDS budget (16-lane kernel)");
+static_assert(kW_Zfin + 16384 == kW_Z1024 && kW_Z1024 + 4096 == kTablesWPlainBytes, "FsTablesW plain layout");
+static_assert(kW_RegionA < 65536, "ds_read offset field");
+constexpr uint32_t kLdsAlloc = kLdsBytes > kW_LdsBytes ? kLdsBytes : kW_LdsBytes;
+
+// The workgroup's LDS image (static allocation of the digest kernels). Namespace scope, so the
 // out-of-line parse routine addresses it as LDS (ds_read), not through a flat pointer.
-__shared__ __attribute__((aligned(16))) char g_lds[kLdsBytes];
+__shared__ __attribute__((aligned(16))) char g_lds[kLdsAlloc];
 
 #ifdef FS_STAMPS
 // Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
@@ -189,17 +211,19 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
-// Z64(a) ^ w from replicated region A. Conflict-free.
+// Z_stride(a) ^ w from replicated region A (Z64 in the 4-lane kernels, Z256 in the 16-lane one).
+// Conflict-free.
+template <uint32_t kRegion = kLdsRegionA>
 __device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const LaneKeys& k, uint32_t w) {
     if (FS_DIAG & 8) {  // diagnostic: the address VALU without the LDS reads (wrong CRC)
         const uint32_t u0 = __builtin_amdgcn_perm(a, k.cvec, k.sel[0]), u1 = __builtin_amdgcn_perm(a, k.cvec, k.sel[1]);
         const uint32_t u2 = __builtin_amdgcn_perm(a, k.cvec, k.sel[2]), u3 = __builtin_amdgcn_perm(a, k.cvec, k.sel[3]);
         return xor3(xor3(u0, u1, u2), u3, w);
     }
-    uint32_t t0 = lds32(lds, kLdsRegionA + __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
-    uint32_t t1 = lds32(lds, kLdsRegionA + __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
-    uint32_t t2 = lds32(lds, kLdsRegionA + __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
-    uint32_t t3 = lds32(lds, kLdsRegionA + __builtin_amdgcn_perm(a, k.cvec, k.sel[3]));
+    uint32_t t0 = lds32(lds, kRegion + __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
+    uint32_t t1 = lds32(lds, kRegion + __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
+    uint32_t t2 = lds32(lds, kRegion + __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
+    uint32_t t3 = lds32(lds, kRegion + __builtin_amdgcn_perm(a, k.cvec, k.sel[3]));
     return xor3(xor3(t0, t1, t2), t3, w);
 }
 
@@ -233,17 +257,18 @@ __device__ __forceinline__ uint32_t range_mask(int k, int a0, int a1) {
 // ---------------------------------------------------------------------------------------
 // Rows.
 
-// A lean row: four Z64 steps and four v_sad_u16, no masks.
+// A lean row: four Z_stride steps and four v_sad_u16, no masks.
+template <uint32_t kRegion = kLdsRegionA>
 __device__ __forceinline__ void lean_row(const char* lds, const LaneKeys& k, u32x4 v, uint32_t (&A)[4], uint32_t& cs) {
     if (FS_DIAG & 4) {  // diagnostic: no table lookups (wrong CRC; the loads and the sum stay)
         A[0] = xor3(A[0], v.x, A[1]); A[1] ^= v.y; A[2] ^= v.z; A[3] ^= v.w;
         cs = sad16(v.x, cs); cs = sad16(v.y, cs); cs = sad16(v.z, cs); cs = sad16(v.w, cs);
         return;
     }
-    A[0] = zrep(lds, A[0], k, v.x);
-    A[1] = zrep(lds, A[1], k, v.y);
-    A[2] = zrep(lds, A[2], k, v.z);
-    A[3] = zrep(lds, A[3], k, v.w);
+    A[0] = zrep<kRegion>(lds, A[0], k, v.x);
+    A[1] = zrep<kRegion>(lds, A[1], k, v.y);
+    A[2] = zrep<kRegion>(lds, A[2], k, v.z);
+    A[3] = zrep<kRegion>(lds, A[3], k, v.w);
     cs = sad16(v.x, cs);
     cs = sad16(v.y, cs);
     cs = sad16(v.z, cs);
@@ -256,6 +281,7 @@ __device__ __forceinline__ void lean_row(const char* lds, const LaneKeys& k, u32
 // nd: frame dwords (0 = nothing to stream); sa: S & 3; tail_mask: bytes of dword nd-1 inside
 // the frame. The head mask (bytes of dword 0 inside the frame) is also the CRC init's part in
 // dword 0; its complement is the init's part in dword 1.
+template <uint32_t kRegion = kLdsRegionA>
 __device__ __forceinline__ void masked_row(const char* lds, const LaneKeys& k, u32x4 u, int rel, int p, int nd,
                                            uint32_t sa, uint32_t tail_mask, uint32_t (&A)[4], uint32_t& cs) {
     const uint32_t head_mask = 0xffffffffu << (8u * sa);
@@ -273,7 +299,7 @@ __device__ __forceinline__ void masked_row(const char* lds, const LaneKeys& k, u
         if (x == 0) { d &= head_mask; c = head_mask; }
         if (x == 1) c = ~head_mask;
         if (x == nd - 1) d &= tail_mask;
-        A[j] = zrep(lds, A[j], k, d ^ c);
+        A[j] = zrep<kRegion>(lds, A[j], k, d ^ c);
         cs = sad16(d, cs);
     }
 }
@@ -290,6 +316,16 @@ __device__ __forceinline__ uint32_t hdr_dw(const char* lds, uint32_t hw, uint32_
 // frame bytes [4j, 4j+4) as a little-endian dword (slot dwords are absolute, sa = S & 3)
 __device__ __forceinline__ uint32_t frame_dw(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t j) {
     return __builtin_amdgcn_alignbyte(hdr_dw(lds, hw, g, j + 1), hdr_dw(lds, hw, g, j), sa);
+}
+
+// frame_dw for a slot of kSlotDw dwords: dwords past the slot come from global memory,
+// clamped to the frame's last dword `last` as the DMA clamps them.
+template <int kSlotDw>
+__device__ __forceinline__ uint32_t frame_dw_t(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t j,
+                                               const uint32_t* fb, uint32_t last) {
+    if (kSlotDw >= 32 || j + 1 < (uint32_t)kSlotDw) return frame_dw(lds, hw, g, sa, j);
+    const uint32_t a = fb[min(j, last)], b = fb[min(j + 1u, last)];
+    return __builtin_amdgcn_alignbyte(b, a, sa);
 }
 
 // Sum, in the accumulator's 16-bit-half domain, of frame bytes [p0, p1) held in the slot's
@@ -335,7 +371,7 @@ struct Parsed {
 // compare the two). Reads only the LDS header slot; `hsum` = sum of frame bytes [0, off)
 // and `pad` = sum of the Ethernet padding [end, len), both from the group-vectorised sums
 // (pad < 0: the padding lies past the slot, summed here from global memory).
-template <uint32_t kOps>
+template <uint32_t kOps, int kSlotDw = kHdrDwords>
 __device__ __forceinline__ Parsed parse_frame(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t len, uint32_t mtu,
                               uint32_t hsum, int64_t pad, const uint32_t* fb) {
     Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0, 0u};
@@ -370,7 +406,8 @@ __device__ __forceinline__ Parsed parse_frame(const char* lds, uint32_t hw, uint
     const uint32_t q = (off - 2u) >> 2;
     uint32_t lb[6];
 #pragma unroll
-    for (uint32_t i = 0; i < 6; ++i) lb[i] = __builtin_bswap32(frame_dw(lds, hw, g, sa, q + i));
+    for (uint32_t i = 0; i < 6; ++i)
+        lb[i] = __builtin_bswap32(frame_dw_t<kSlotDw>(lds, hw, g, sa, q + i, fb, ((sa + len + 3u) >> 2) - 1u));
     const uint32_t sport = lb[0] & 0xffffu, dport = lb[1] >> 16;
     uint32_t lenword;
     if (proto == 17u) {                                                       // :222-244
@@ -455,23 +492,27 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, ui
 // call saves nothing). Every lane takes part: group-vectorised sums over the header slot
 // (the bytes [0, off) of the Ethernet + IP headers; the Ethernet padding [end, len) when it
 // lies in the slot), then the parser lane's gates and corrections, parked in LDS.
-template <uint32_t kOps>
+// `pk`: where the parse result is parked (the 4-lane kernels park it in the header slot itself).
+template <uint32_t kOps, int kSlotDw = kHdrDwords>
 __device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
-                                                     uint32_t mtu, const uint32_t* fbs, bool parser) {
+                                                     uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk) {
     const char* lds = g_lds;
     const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3));
     const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
     const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 4)) >> 16;
     const uint32_t end = (14u + tl) & 0xffffu;
-    // [0, off) spans at most 3 + 74 bytes: absolute dwords < 20
-    const uint32_t hsum = slot_sum(lds, hw, grp, gl, sa, 0, (int)min(off, len), 5);
-    const bool pad_in_slot = sa + len <= 4u * kHdrDwords;
+    // [0, off) spans at most 3 + 74 bytes: absolute dwords < 20 (a 16-dword slot holds [0, 64 - sa);
+    // longer IP headers are summed from global memory)
+    const uint32_t h1 = min(off, len);
+    uint32_t hsum = slot_sum(lds, hw, grp, gl, sa, 0, (int)h1, min(5, kSlotDw / 4));
+    if (kSlotDw < 32 && sa + h1 > 4u * kSlotDw) hsum = global_sum(fbs, sa, 0, (int)h1);
+    const bool pad_in_slot = sa + len <= 4u * kSlotDw;
     int64_t pad = -1;
     if (__ballot(len >= 34u && end < len && pad_in_slot) != 0) {
-        const uint32_t ps = slot_sum(lds, hw, grp, gl, sa, (int)min(end, len), (int)len, kHdrDwords / 4);
+        const uint32_t ps = slot_sum(lds, hw, grp, gl, sa, (int)min(end, len), (int)len, kSlotDw / 4);
         if (pad_in_slot) pad = (int64_t)ps;
     }
-    if (parser) park_parsed<kOps>(g_lds, hw, grp, parse_frame<kOps>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
+    if (parser) park_parsed<kOps>(g_lds, pk, grp, parse_frame<kOps, kSlotDw>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
 }
 
 // Final L4 checksum + verdict (parser lane) once the streamed sum is known.
@@ -520,7 +561,13 @@ __device__ __forceinline__ void st8(uint8_t* p, uint32_t v) { *p = (uint8_t)v; }
 // The parser lane's finish of one frame: CRC-32 from the combined register Y, L4 checksum and
 // verdict from the streamed sum `cs` and the parked parse, then the op's writes and stores.
 // `len` is the frame length the rows streamed (kOpsFcs: without the FCS).
-template <uint32_t kOps>
+// The table layout of the 4-lane kernels, for the finish (LayoutW: the 16-lane kernel).
+struct LayoutA {
+    static constexpr uint32_t kZfin = kLdsZfin;
+    __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift(lds, v, k); }
+};
+
+template <uint32_t kOps, class L = LayoutA>
 __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, uint64_t S, uint32_t len,
                                              uint32_t te, uint32_t Y, uint32_t cs, const uint8_t* frames,
                                              uint8_t* wframes, const uint32_t* lengths, uint32_t fi, uint2* out,
@@ -537,11 +584,11 @@ __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, u
         uint32_t c = 0xffffffffu;
         const uint8_t* fbytes = frames + S;
         for (uint32_t p = 0; p < len; ++p)
-            c = lds32(lds, kLdsZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
+            c = lds32(lds, L::kZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
         crcv = ~c;
     } else {
         const uint32_t tpad = (4u - te) & 3u;  // zero bytes appended by the dword rounding
-        crcv = ~zplain(lds, Y, kLdsZfin + 4096u * tpad);
+        crcv = ~zplain(lds, Y, L::kZfin + 4096u * tpad);
     }
     uint32_t verdict = P.verdict, l4 = 0u;
     if (P.compute) l4 = finish_l4(fbs, sa, len, P, cs, verdict);
@@ -553,8 +600,8 @@ __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, u
             // of the two 16-bit XOR deltas: Z_(len-p2)( Z_(p2-24)(d_ip) ^ d_l4 ), d as LE bytes
             const uint32_t ipc = P.ip_csum, old_ip = P.aux & 0xffffu, p2 = P.aux >> 16;
             if (!(FS_TXDIAG & 1)) {
-                const uint32_t d = zshift(lds, bswap16(old_ip ^ ipc), p2 - 24u) ^ bswap16(P.stored ^ l4);
-                crcv ^= zshift(lds, d, len - p2);
+                const uint32_t d = L::shift(lds, bswap16(old_ip ^ ipc), p2 - 24u) ^ bswap16(P.stored ^ l4);
+                crcv ^= L::shift(lds, d, len - p2);
             }
             if (!(FS_TXDIAG & 2)) {
                 st8(wf + 24, ipc >> 8);
@@ -1135,7 +1182,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetchA);
             else __builtin_amdgcn_s_waitcnt(0x0070);
             parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
-                       parser);
+                       parser, hw);
         };
         auto prio = [&](int r0) {
             // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
@@ -1344,7 +1391,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetch);
             else __builtin_amdgcn_s_waitcnt(0x0070);
             parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
-                       parser);
+                       parser, hw);
         };
         uint32_t Y = 0u, csum = 0u;  // the frame's combined register value and sum (mode A)
         for (int pass = 0; pass < npass; ++pass) {
@@ -1489,8 +1536,508 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     }
 }
 
+
+// =======================================================================================
+// The 16-lane kernel (digest_kernel_w).
+//
+// A wave owns a SUPER-TILE of 16 consecutive frames (8 or 4 for small batches). The header
+// DMA, the parse and the finish work on it as the 4-lane kernels do (4 lanes per frame). The
+// rows stream in PASSES of 4 frames with a GROUP of 16 lanes per frame: 256-byte rows
+// anchored at the frame's dword-rounded end, lane j of the group loading dwords [4j, 4j+4)
+// of every row (16 B/lane, a 256-B contiguous piece per frame per load instruction -- the
+// access pattern that reads at the plain-stream rate, tools/tile_pattern.hip). The frames are
+// ordered by row count into the passes, so a pass holds frames of similar length. Each lane
+// keeps 4 dword streams with A <- Z256(A) ^ w (region A holds Z_256); a pass ends with the
+// 64-stream combine of each frame (Z12/Z8/Z4 within a lane, Z48/Z32/Z16 within a quad of
+// lanes, Z192/Z128/Z64 across the quads), parked per frame in LDS for the finish.
+// One ring of kPfW row loads runs through the whole launch: a pass's last block refills the
+// ring with the next pass's (or the next super-tile's) first rows, so the loads never drain
+// between passes. The next super-tile's descriptors are loaded one super-tile ahead, its
+// geometry (ordering, rows per pass) and header DMA are set up at the current super-tile's
+// last block.
+
+#ifndef FS_PREFETCH_W
+#define FS_PREFETCH_W 3
+#endif
+#ifdef FS_DIAG_W_DUMP
+__device__ uint32_t g_wdump[kTablesWLdsBytes / 4];
+#endif
+constexpr int kPfW = FS_PREFETCH_W;
+constexpr int kRowDwW = 64;  // 256-byte rows
+
+__device__ __forceinline__ uint32_t zshift_w(const char* lds, uint32_t v, uint32_t k) {
+    for (; k >= 1024u; k -= 1024u) v = zplain(lds, v, kW_Z1024);
+    for (; k >= 256u; k -= 256u)
+        v = lds32(lds, kW_RegionA + ((v & 0xffu) << 8)) ^ lds32(lds, kW_RegionA + (((v >> 8) & 0xffu) << 8) + 32u) ^
+            lds32(lds, kW_RegionA + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kW_RegionA + ((v >> 24) << 8) + 96u);
+    if (k >= 192u) { v = zplain(lds, v, kW_Z192); k -= 192u; }
+    else if (k >= 128u) { v = zplain(lds, v, kW_Z128); k -= 128u; }
+    else if (k >= 64u) { v = zplain(lds, v, kW_Z64); k -= 64u; }
+    if (k >= 48u) { v = zplain(lds, v, kW_Z48); k -= 48u; }
+    else if (k >= 32u) { v = zplain(lds, v, kW_Z32); k -= 32u; }
+    else if (k >= 16u) { v = zplain(lds, v, kW_Z16); k -= 16u; }
+    if (k >= 12u) { v = zplain(lds, v, kW_Z12); k -= 12u; }
+    else if (k >= 8u) { v = zplain(lds, v, kW_Z8); k -= 8u; }
+    else if (k >= 4u) { v = zplain(lds, v, kW_Zfin); k -= 4u; }
+    if (k > 0u) v = zplain(lds, v, kW_Zfin + 4096u * (4u - k));
+    return v;
+}
+
+struct LayoutW {
+    static constexpr uint32_t kZfin = kW_Zfin;
+    __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift_w(lds, v, k); }
+};
+
+// Region A (Z_256, 8 copies per byte table) in place: thread t writes the 16-B chunk t & 7 of
+// entry rows t >> 3 and 128 + (t >> 3); the 8 lanes of a ds_write_b128 lane group fill one
+// entry row's 128 bytes, so the stores are bank-conflict-free. The basis (32 dwords) comes in
+// by two scalar loads; each lane selects its byte table's 8 columns.
+__device__ __forceinline__ void build_region_w(const FsTablesW* __restrict__ tabs, char* lds) {
+    typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+    const uint32_t t = threadIdx.x;
+    const uint32_t c = t & 7u, b = c >> 1, e = t >> 3;
+    const uint64_t a = reinterpret_cast<uint64_t>(&tabs->z256_basis[0][0]);
+    const uint64_t sa = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    u32x16 lo, hi;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(lo), "=s"(hi)
+                 : "s"(sa));
+    // branch-free selection of the byte table's columns (a select chain on the lane's table
+    // index was lowered to divergent control flow that picked wrong SGPRs for table 3)
+    const uint32_t m1 = 0u - (b & 1u), m2 = 0u - ((b >> 1) & 1u);
+    uint32_t v = 0, col7 = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t a0 = (lo[j] & ~m1) | (lo[8 + j] & m1);
+        const uint32_t a1 = (hi[j] & ~m1) | (hi[8 + j] & m1);
+        const uint32_t cj = (a0 & ~m2) | (a1 & m2);
+        if (j < 7) v ^= cj & (0u - ((e >> j) & 1u));
+        else col7 = cj;
+    }
+    *reinterpret_cast<u32x4*>(lds + kW_RegionA + e * 256u + 16u * c) = u32x4{v, v, v, v};
+    const uint32_t v2 = v ^ col7;
+    *reinterpret_cast<u32x4*>(lds + kW_RegionA + (e + 128u) * 256u + 16u * c) = u32x4{v2, v2, v2, v2};
+}
+
+// The plain tables (52 KB): 4 1-KB LDS-DMA pieces per wave.
+__device__ __forceinline__ void plain_dma_w(const FsTablesW* __restrict__ tabs, const char* lds, uint32_t wave,
+                                            uint32_t lane) {
+    constexpr uint32_t kPieces = kTablesWPlainBytes / 1024u;
+    constexpr uint32_t kPer = (kPieces + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint32_t lds0 = lds_base(lds);
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t c = min(w0 + k * kWavesPerBlock, kPieces - 1u);
+        dma_x4(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
+               __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
+    }
+}
+
+// Header slots of a super-tile (4-lane mapping: lane (grp, gl) describes frame grp, S / len
+// its descriptor, len 0 for an empty group): frame dwords [0, 16) in the [x >> 2][frame][x & 3]
+// layout. One dwordx4 DMA when every frame spans the slot, else 4 dword DMAs clamped to each
+// frame's last dword. Returns the DMA instruction count (wave-uniform).
+__device__ __forceinline__ int header_dma_w(uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
+                                            const char* lds, uint32_t hw, uint32_t gl, uint32_t lane) {
+    const uint32_t hdr0 = __builtin_amdgcn_readfirstlane(lds_base(lds) + hw);
+    const uint32_t sa = (uint32_t)S & 3u;
+    const int last = (int)((sa + len + 3u) >> 2) - 1;
+    const bool own = len > 0u;
+    const uint64_t fa = reinterpret_cast<uint64_t>(frames + ((S >> 2) << 2));
+    if (__ballot(own && last < kHdrDwW - 1) == 0) {
+        const int src = (int)((lane & 15u) << 4);  // frame (lane & 15)'s lane 0
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)fa);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(fa >> 32));
+        const uint32_t lg = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
+        const uint32_t* fb = reinterpret_cast<const uint32_t*>(((uint64_t)hi << 32) | lo);
+        if (lg > 0u) dma_x4(fb + 4u * (lane >> 4), hdr0);
+        return 1;
+    }
+    if (own) {
+        const uint32_t* fbs = reinterpret_cast<const uint32_t*>(fa);
+#pragma unroll
+        for (int i = 0; i < kHdrDwW / 4; ++i) dma_x1(fbs + min(4 * i + (int)gl, last), hdr0 + 256u * i);
+    }
+    return kHdrDwW / 4;
+}
+
+// The descriptors of super-tile st into the wave's descriptor area by ONE dword LDS-DMA: lanes
+// 0..31 the 16 offsets (two dwords each), lanes 32..47 the 16 lengths (lanes 48..63 re-read the
+// last length); frames past the batch end read the last frame's descriptor.
+__device__ __forceinline__ void desc_dma_w(uint32_t st, uint32_t n, uint32_t fpt, const uint64_t* __restrict__ offsets,
+                                           const uint32_t* __restrict__ lengths, const char* lds, uint32_t dsc,
+                                           uint32_t lane) {
+    const uint32_t f0 = st * fpt;
+    const uint32_t k = lane < 32u ? lane >> 1 : lane < 48u ? lane - 32u : 15u;
+    const uint32_t fi = min(f0 + min(k, fpt - 1u), n - 1u);
+    const void* src = lane < 32u ? static_cast<const void*>(reinterpret_cast<const uint32_t*>(offsets + fi) + (lane & 1u))
+                                 : static_cast<const void*>(lengths + fi);
+    dma_x1(src, __builtin_amdgcn_readfirstlane(lds_base(lds) + dsc));
+}
+
+// Geometry of a super-tile (4-lane mapping; every lane takes part): the frame table, the
+// frames' order by row count (stable), rows and masked head rows per pass, into geometry
+// buffer gb. S / len: this lane's frame (len already without a trailing FCS).
+__device__ __forceinline__ void setup_st(char* lds, uint32_t gb, uint32_t st, uint32_t grp, uint32_t gl, uint32_t n,
+                                         uint32_t fpt, uint64_t S, uint32_t len) {
+    const bool valid = grp < fpt && st * fpt + grp < n;
+    const uint32_t L = valid ? len : 0u;
+    const uint32_t sa = (uint32_t)S & 3u;
+    const int nd = L >= 4u ? (int)((sa + L + 3u) >> 2) : 0;
+    const int rows = (nd + kRowDwW - 1) / kRowDwW;
+    if (gl == 0u) *reinterpret_cast<u32x4*>(lds + gb + 16u * grp) = u32x4{(uint32_t)S, (uint32_t)(S >> 32), L, (uint32_t)nd};
+    // rank of this frame by (rows, index) among the super-tile's fpt slots (rows read by
+    // readlane); slots past fpt keep their index (they are in no pass)
+    int rank = 0;
+#pragma unroll
+    for (int g = 0; g < kFramesPerTile; ++g) {
+        const int rg = __builtin_amdgcn_readlane(rows, 4 * g);
+        rank += (g < (int)fpt && (rg < rows || (rg == rows && g < (int)grp))) ? 1 : 0;
+    }
+    if (grp >= fpt) rank = (int)grp;
+    if (gl == 0u) *reinterpret_cast<uint8_t*>(lds + gb + kW_GeoOrder + rank) = (uint8_t)grp;
+    const int pass = rank >> 2;
+    const int npass = (int)(fpt >> 2);
+    int Pmine = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int Pp = group_max(pass == p ? rows : 0);
+        const int Pr = (Pp + kPfW - 1) / kPfW * kPfW;
+        if (pass == p) Pmine = Pr;
+        if ((threadIdx.x & 63u) == 0u) *reinterpret_cast<uint32_t*>(lds + gb + kW_GeoP + 4u * p) = (uint32_t)Pr;
+    }
+    const int need = 2 - (nd - kRowDwW * Pmine);
+    const int h = (nd > 0 && need > 0) ? (need + kRowDwW - 1) / kRowDwW : 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int Hp = group_max(pass == p ? h : 0);
+        if ((threadIdx.x & 63u) == 0u) *reinterpret_cast<uint32_t*>(lds + gb + kW_GeoH + 4u * p) = (uint32_t)Hp;
+    }
+    if ((threadIdx.x & 63u) == 0u) *reinterpret_cast<uint32_t*>(lds + gb + kW_GeoNpass) = (uint32_t)npass;
+}
+
+// The rows of one pass for this lane (16-lane mapping: group g16 = lane >> 4, lane j in it).
+struct UnitW {
+    const uint32_t* gfb;  // frame dword 0 of the lane's rows (the pass's longest frame for an empty group)
+    int rel0;             // frame dword of this lane's chunk in row 0
+    int lo;               // lowest frame dword a clamped load may start at
+    int P, H;             // wave-uniform: rows (a multiple of kPfW) and leading masked rows
+    int nd;               // the group's own frame: stream dwords (0 = empty or under 4 bytes)
+    uint32_t sa;          // its start alignment
+    uint32_t tail_mask;   // bytes of its last dword inside the frame
+};
+
+__device__ __forceinline__ UnitW unit_w(const char* lds, uint32_t gb, int p, uint32_t g16, uint32_t j,
+                                        const uint8_t* __restrict__ frames) {
+    UnitW U;
+    U.P = (int)__builtin_amdgcn_readfirstlane(lds32(lds, gb + kW_GeoP + 4u * (uint32_t)p));
+    U.H = (int)__builtin_amdgcn_readfirstlane(lds32(lds, gb + kW_GeoH + 4u * (uint32_t)p));
+    const uint32_t f = *reinterpret_cast<const uint8_t*>(lds + gb + kW_GeoOrder + 4u * (uint32_t)p + g16);
+    const uint32_t fm = *reinterpret_cast<const uint8_t*>(lds + gb + kW_GeoOrder + 4u * (uint32_t)p + 3u);
+    const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * f);
+    const u32x4 dm = *reinterpret_cast<const u32x4*>(lds + gb + 16u * fm);
+    U.nd = (int)d.w;
+    const uint64_t S = ((uint64_t)d.y << 32) | d.x;
+    U.sa = (uint32_t)S & 3u;
+    const uint32_t e = (U.sa + d.z) & 3u;
+    U.tail_mask = e ? ((1u << (8u * e)) - 1u) : 0xffffffffu;
+    const bool own = U.nd > 0;
+    const uint64_t ls = own ? S : (((uint64_t)dm.y << 32) | dm.x);
+    const int lnd = own ? U.nd : (int)dm.w;
+    const uint64_t sdw = ls >> 2;
+    U.gfb = reinterpret_cast<const uint32_t*>(frames + (sdw << 2));
+    U.rel0 = lnd - kRowDwW * U.P + 4 * (int)j;
+    U.lo = max(sdw > (1u << 24) ? -(1 << 24) : -(int)sdw, min(0, lnd - 4));
+    return U;
+}
+
+__device__ __forceinline__ void prefetch_w(const UnitW& U, u32x4 (&pf)[kPfW]) {
+#pragma unroll
+    for (int i = 0; i < kPfW; ++i) {
+        const int rel = U.rel0 + kRowDwW * i;
+        pf[i] = load_row(U.gfb, i < U.H ? load_pos(rel, U.lo) : rel);
+    }
+}
+
+// The 64-stream combine of a pass (16-lane mapping): U = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3 ^ junk
+// per lane, Z_(16(3 - (j & 3))) per lane and a quad XOR, Z_(64(3 - (j >> 2))) per quad and an
+// XOR over the quads (DPP row_ror 4 and 8); the checksum partials folded and summed likewise.
+__device__ __forceinline__ void combine_w(const char* lds, uint32_t j, const uint32_t (&A)[4], uint32_t cs,
+                                          uint32_t junk, uint32_t& Y, uint32_t& csum) {
+    const uint32_t U = zplain(lds, A[0], kW_Z12) ^ zplain(lds, A[1], kW_Z8) ^ zplain(lds, A[2], kW_Zfin) ^ A[3] ^ junk;
+    cs -= sad16(junk, 0u);
+    const uint32_t w = j & 3u, q = j >> 2;
+    uint32_t y = zplain(lds, U, w == 0u ? kW_Z48 : w == 1u ? kW_Z32 : kW_Z16);
+    if (w == 3u) y = U;
+    y ^= dpp_quad<kQuadXor1>(y);
+    y ^= dpp_quad<kQuadXor2>(y);
+    uint32_t z = zplain(lds, y, q == 0u ? kW_Z192 : q == 1u ? kW_Z128 : kW_Z64);
+    if (q == 3u) z = y;
+    z ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)z, 0x124, 0xf, 0xf, false);  // row_ror:4
+    z ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)z, 0x128, 0xf, 0xf, false);  // row_ror:8
+    cs = (cs & 0xffffu) + (cs >> 16);
+    cs += dpp_quad<kQuadXor1>(cs);
+    cs += dpp_quad<kQuadXor2>(cs);
+    cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0x124, 0xf, 0xf, false);
+    cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0x128, 0xf, 0xf, false);
+    Y = z;
+    csum = cs;
+}
+
+// vmcnt(N) tied to registers loaded by inline asm (no use is scheduled above it).
+template <int N>
+__device__ __forceinline__ void wait_tied(uint64_t& S, uint32_t& len) {
+    if (N == 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(S), "+v"(len));
+    else asm volatile("s_waitcnt vmcnt(%2)" : "+v"(S), "+v"(len) : "n"(N));
+}
+
+template <uint32_t kOps>
+__global__ void __launch_bounds__(kThreads, 1)
+digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+                const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTablesW* __restrict__ tabs,
+                uint2* __restrict__ out, uint8_t* __restrict__ status, uint8_t* wframes, uint32_t tx, uint32_t fpt) {
+    char* lds = g_lds;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+    fpt = __builtin_amdgcn_readfirstlane(fpt);
+    const uint32_t nst = (n + fpt - 1) / fpt;
+    const uint32_t hw = kW_Hdr + wave * kHdrWaveW;
+    const uint32_t wb = kW_Wave + wave * kW_WaveBytes;
+    const uint32_t pk = wb + kW_Park;
+
+    LaneKeys keys;
+    {
+        const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
+        keys.cvec = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) keys.cvec |= (32u * j + 4u * c) << (8u * j);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t b = (k + h) & 3u;
+            keys.sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
+        }
+    }
+
+    uint32_t st = wave * gridDim.x + blockIdx.x;  // wave-major first super-tile
+    u32x4 pf[kPfW];
+    const uint32_t dsc = wb + kW_Desc;  // the next super-tile's descriptors, DMA'd one super-tile ahead
+    uint32_t gb = wb + kW_Geo;  // geometry buffer of the super-tile being consumed
+    bool pre = false;           // the current pass's first rows are in the ring
+    {
+        const uint32_t grp = lane >> 2, gl = lane & 3u;
+        uint64_t S = 0;
+        uint32_t len = 0;
+        const bool first = st < nst;
+        if (first) tile_descriptors(st, grp, n, offsets, lengths, S, len, fpt);
+        plain_dma_w(tabs, lds, wave, lane);
+#ifdef FS_DIAG_W_DMA_A
+        {  // diagnostic: region A copied from the host-built image instead of built in place
+            const uint32_t lds0 = lds_base(lds);
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t c = wave + 16u * k;
+                dma_x4(reinterpret_cast<const char*>(tabs) + kTablesWPlainBytes + c * 1024u + lane * 16u,
+                       __builtin_amdgcn_readfirstlane(lds0 + kW_RegionA + c * 1024u));
+            }
+        }
+#else
+        build_region_w(tabs, lds);
+#endif
+        wait_tied<0>(S, len);
+        if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
+        if (first) {
+            setup_st(lds, gb, st, grp, gl, n, fpt, S, len);
+            const bool valid = grp < fpt && st * fpt + grp < n;
+            header_dma_w(S, valid ? len : 0u, frames, lds, hw, gl, lane);
+            if (st + nwaves < nst) desc_dma_w(st + nwaves, n, fpt, offsets, lengths, lds, dsc, lane);
+            const UnitW U0 = unit_w(lds, gb, 0, lane >> 4, lane & 15u, frames);
+            if (U0.P > 0) {
+                prefetch_w(U0, pf);
+                pre = true;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): region A and the geometry are in LDS
+        __builtin_amdgcn_s_barrier();        // tables ready (no vmcnt drain)
+#ifdef FS_DIAG_W_DUMP
+        if (blockIdx.x == 0) {  // diagnostic: workgroup 0's table image
+            for (uint32_t i = threadIdx.x; i < kTablesWLdsBytes / 4; i += kThreads)
+                g_wdump[i] = lds32(lds, 4u * i);
+        }
+#endif
+        if (FS_AGE_PRIO) {
+            const uint32_t w = wave >> 2;
+            if (w == 3u) __builtin_amdgcn_s_setprio(3);
+            else if (w == 2u) __builtin_amdgcn_s_setprio(2);
+            else if (w == 1u) __builtin_amdgcn_s_setprio(1);
+        }
+    }
+
+    while (st < nst) {
+        const int npass = (int)__builtin_amdgcn_readfirstlane(lds32(lds, gb + kW_GeoNpass));
+        const uint32_t gnext = gb == wb + kW_Geo ? wb + kW_Geo + kW_GeoBytes : wb + kW_Geo;  // the other buffer
+        bool parsed = false, next_ready = false;
+        // header parse of the whole super-tile (4-lane mapping), once the header DMA has landed:
+        // it was issued before this super-tile's first rows
+        auto parse = [&](bool refilled) {
+            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfW);
+            else __builtin_amdgcn_s_waitcnt(0x0070);
+            uint32_t ln;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+            const uint32_t grp = ln >> 2, gl = ln & 3u;
+            const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * grp);
+            const uint64_t S = ((uint64_t)d.y << 32) | d.x;
+            const bool valid = grp < fpt && st * fpt + grp < n;
+            parse_tile<kOps, kHdrDwW>(hw, grp, gl, (uint32_t)S & 3u, d.z, mtu,
+                                      reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), valid && gl == 0u, pk);
+            parsed = true;
+        };
+        // the next super-tile: geometry, header DMA, the descriptors of the one after, its first unit
+        auto setup_next = [&](bool in_block) -> UnitW {
+            // the descriptor DMA is older than the ring's kPfW youngest loads (or than everything)
+            if (in_block) __builtin_amdgcn_s_waitcnt(0x0070 | kPfW);
+            else __builtin_amdgcn_s_waitcnt(0x0070);
+            const uint32_t grp = lane >> 2, gl = lane & 3u;
+            const uint64_t S = *reinterpret_cast<const uint64_t*>(lds + dsc + 8u * grp);
+            uint32_t len = *reinterpret_cast<const uint32_t*>(lds + dsc + kW_DescLen + 4u * grp);
+            if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
+            const uint32_t stn = st + nwaves;
+            setup_st(lds, gnext, stn, grp, gl, n, fpt, S, len);
+            const bool valid = grp < fpt && stn * fpt + grp < n;
+            header_dma_w(S, valid ? len : 0u, frames, lds, hw, gl, lane);
+            if (stn + nwaves < nst) desc_dma_w(stn + nwaves, n, fpt, offsets, lengths, lds, dsc, lane);
+            next_ready = true;
+            return unit_w(lds, gnext, 0, lane >> 4, lane & 15u, frames);
+        };
+
+        for (int p = 0; p < npass; ++p) {
+            const uint32_t j = lane & 15u;
+            const UnitW U = unit_w(lds, gb, p, lane >> 4, j, frames);
+            uint32_t A[4] = {0u, 0u, 0u, 0u};
+            uint32_t cs = 0u;
+            if (U.P > 0 && !pre) prefetch_w(U, pf);
+            pre = false;
+            const uint32_t tail_mask = U.tail_mask;
+            // general block: rows below H masked; refill 0 none, 1 this unit, 2 the next unit
+            uint32_t lastw = 0u;  // the pass's last row's last dword, kept before its slot is refilled
+            auto block = [&](int r0, const UnitW& Un, auto kind_tag) {
+                constexpr int kKind = decltype(kind_tag)::value;
+#pragma unroll
+                for (int i = 0; i < kPfW; ++i) {
+                    const int r = r0 + i;
+                    const int rel = U.rel0 + kRowDwW * r;
+                    if (r < U.H) masked_row<kW_RegionA>(lds, keys, pf[i], rel, load_pos(rel, U.lo), U.nd, U.sa, tail_mask, A, cs);
+                    else lean_row<kW_RegionA>(lds, keys, pf[i], A, cs);
+                    if (kKind != 1 && i == kPfW - 1) lastw = pf[i].w;
+                    if (kKind == 1) {
+                        const int rn = rel + kRowDwW * kPfW;
+                        pf[i] = load_row(U.gfb, r + kPfW < U.H ? load_pos(rn, U.lo) : rn);
+                    } else if (kKind == 2) {
+                        const int rn = Un.rel0 + kRowDwW * i;
+                        pf[i] = load_row(Un.gfb, i < Un.H ? load_pos(rn, Un.lo) : rn);
+                    }
+                }
+            };
+            auto lean_block = [&](int r0, const UnitW& Un, auto kind_tag) {
+                constexpr int kKind = decltype(kind_tag)::value;
+                const uint32_t* pb = U.gfb + (U.rel0 + kRowDwW * (r0 + kPfW));
+#pragma unroll
+                for (int i = 0; i < kPfW; ++i) {
+                    lean_row<kW_RegionA>(lds, keys, pf[i], A, cs);
+                    if (kKind != 1 && i == kPfW - 1) lastw = pf[i].w;
+                    if (kKind == 1) {
+                        pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwW * i);
+                    } else if (kKind == 2) {
+                        const int rn = Un.rel0 + kRowDwW * i;
+                        pf[i] = load_row(Un.gfb, i < Un.H ? load_pos(rn, Un.lo) : rn);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            };
+            using K0 = std::integral_constant<int, 0>;
+            using K1 = std::integral_constant<int, 1>;
+            using K2 = std::integral_constant<int, 2>;
+            for (int r0 = 0; r0 < U.P; r0 += kPfW) {
+                const bool lastb = r0 + kPfW == U.P;
+                if (!lastb) {
+                    if (r0 >= U.H) lean_block(r0, U, K1());
+                    else block(r0, U, K1());
+                    if (!parsed) parse(true);
+                    continue;
+                }
+                // the last block of the pass refills the ring with the next unit's first rows
+                UnitW Un;
+                Un.P = 0;
+                if (p + 1 < npass) {
+                    Un = unit_w(lds, gb, p + 1, lane >> 4, j, frames);
+                } else if (st + nwaves < nst) {
+                    // the next super-tile's header DMA rewrites the slot: parse this one first
+                    if (!parsed) parse(false);
+                    Un = setup_next(true);
+                }
+                if (Un.P > 0) {
+                    pre = true;
+                    if (r0 >= U.H) lean_block(r0, Un, K2());
+                    else block(r0, Un, K2());
+                    if (!parsed) parse(true);
+                } else {
+                    if (r0 >= U.H) lean_block(r0, Un, K0());
+                    else block(r0, Un, K0());
+                    if (!parsed) parse(false);
+                }
+            }
+            // combine the pass: the last row was lean unless every row was masked; its last
+            // dword (lane 15's 4th) still holds the up to 3 bytes past the frame end
+            uint32_t junk = 0u;
+            if (U.P > 0 && U.H < U.P && j == 15u && U.nd > 0) junk = lastw & ~tail_mask;
+            if (U.P == 0) {
+                A[0] = A[1] = A[2] = A[3] = 0u;
+                cs = 0u;
+            }
+            uint32_t Y, csum;
+            combine_w(lds, j, A, cs, junk, Y, csum);
+            if (j == 0u) {
+                const uint32_t f = *reinterpret_cast<const uint8_t*>(lds + gb + kW_GeoOrder + 4u * (uint32_t)p + (lane >> 4));
+                *reinterpret_cast<uint2*>(lds + wb + kW_Ycs + 8u * f) = make_uint2(Y, csum);
+            }
+        }
+        if (!parsed) parse(false);
+        if (!next_ready && st + nwaves < nst) {
+            const UnitW Un = setup_next(false);
+            if (Un.P > 0) {
+                prefetch_w(Un, pf);
+                pre = true;
+            }
+        }
+        // ---- finish the super-tile (4-lane mapping: the group's lane 0 finishes its frame)
+        {
+            uint32_t ln;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+            const uint32_t grp = ln >> 2, gl = ln & 3u;
+            const bool valid = grp < fpt && st * fpt + grp < n;
+            if (valid && gl == 0u) {
+                const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * grp);
+                const uint64_t S = ((uint64_t)d.y << 32) | d.x;
+                const uint32_t len = d.z;
+                const uint32_t e = (((uint32_t)S & 3u) + len) & 3u;
+                const uint2 yc = *reinterpret_cast<const uint2*>(lds + wb + kW_Ycs + 8u * grp);
+                finish_frame<kOps, LayoutW>(lds, unpark_parsed<kOps>(lds, pk, grp), S, len, e ? e : 4u, yc.x, yc.y,
+                                            frames, wframes, lengths, st * fpt + grp, out, status, tx);
+            }
+        }
+        st += nwaves;
+        gb = gnext;
+    }
+}
+
 }  // namespace
 
+#ifdef FS_DIAG_W_DUMP
+extern "C" int fs_debug_read_wdump(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wdump), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 #ifdef FS_STAMPS
 extern "C" int fs_debug_read_stamps(void* host, size_t bytes) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fs_stamps), bytes, 0, hipMemcpyDeviceToHost);
@@ -1500,7 +2047,7 @@ extern "C" int fs_debug_read_stamps(void* host, size_t bytes) {
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
                          int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force, FsOp op,
-                         uint8_t* wframes, uint32_t tx) {
+                         uint8_t* wframes, uint32_t tx, const FsTablesW* tables_w) {
     if (n == 0) return hipSuccess;
     const uint32_t max_blocks = (uint32_t)(num_cus > 0 ? num_cus : 256);
     // The report of the launches before (the latest launch id that met a mixed-length tile):
@@ -1531,6 +2078,18 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     uint32_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     uint2* o = reinterpret_cast<uint2*>(out);
+    if ((force == 0 || force == 3) && tables_w) {
+#define FS_LAUNCH_W(OPS)                                                                                       \
+    hipLaunchKernelGGL((digest_kernel_w<OPS>), dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, \
+                       mtu, tables_w, o, status, wframes, tx, fpt)
+        switch (op) {
+        case FsOp::kDigest: FS_LAUNCH_W(kOpsDigest); break;
+        case FsOp::kFill: FS_LAUNCH_W(kOpsTx); break;
+        case FsOp::kFcs: FS_LAUNCH_W(kOpsFcs); break;
+        }
+#undef FS_LAUNCH_W
+        return hipGetLastError();
+    }
 #define FS_LAUNCH(K, OPS)                                                                                   \
     hipLaunchKernelGGL((K<OPS>), dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)

@@ -147,3 +147,60 @@ def fold_native_to_be(total: int, parity: int) -> int:
     if not parity:
         r = ((r & 0xFF) << 8) | (r >> 8)
     return r
+
+
+# ---- the wide-group kernel (digest_kernel_w): 16 lanes per frame, end-anchored 256-byte rows,
+# A <- Z256(A) ^ w per dword stream, the combine U = Z12(A0)^Z8(A1)^Z4(A2)^A3 per lane, then
+# Z_(16(3-(j&3))) per lane and a quad XOR, then Z_(64(3-(j>>2))) per quad and an XOR over the
+# quads, then the final Z_(4-t).
+Z256, Z12, Z8, Z48 = op_table(256), op_table(12), op_table(8), op_table(48)
+Z64Q, Z128, Z192 = Z64, op_table(128), op_table(192)
+
+
+def crc32_model_w(buf: bytes, S: int, length: int) -> int:
+    E = S + length
+    if length < 4:
+        return crc32_model(buf, S, length)
+    sdw = S >> 2
+    nd = ((E + 3) >> 2) - sdw
+    sa = S & 3
+    te = (E & 3) or 4
+    head_mask = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
+    tail_mask = 0xFFFFFFFF if te == 4 else (1 << (8 * te)) - 1
+    padded = bytes(buf) + b"\0" * 8
+
+    def dword(rel):
+        return struct.unpack_from("<I", padded, 4 * (sdw + rel))[0]
+
+    R = (nd + 63) // 64
+    A = [[0] * 4 for _ in range(16)]
+    for r in range(R):
+        for lane in range(16):
+            rel = nd - 64 * R + 64 * r + 4 * lane
+            for j in range(4):
+                rj = rel + j
+                dc = 0
+                if rj >= 0:
+                    mk, x = 0xFFFFFFFF, 0
+                    if rj == 0:
+                        mk &= head_mask
+                        x ^= head_mask
+                    if rj == 1:
+                        x ^= (~head_mask) & 0xFFFFFFFF
+                    if rj == nd - 1:
+                        mk &= tail_mask
+                    dc = (dword(rj) & mk) ^ x
+                A[lane][j] = apply(Z256, A[lane][j]) ^ dc
+    quad_tab = [Z48, Z32, Z16, None]
+    quad_level = [Z192, Z128, Z64Q, None]
+    Y = 0
+    for q in range(4):
+        W = 0
+        for w in range(4):
+            lane = 4 * q + w
+            a = A[lane]
+            u = apply(Z12, a[0]) ^ apply(Z8, a[1]) ^ apply(Z4, a[2]) ^ a[3]
+            W ^= u if quad_tab[w] is None else apply(quad_tab[w], u)
+        Y ^= W if quad_level[q] is None else apply(quad_level[q], W)
+    t = (4 - (E & 3)) & 3
+    return apply(ZFIN[t], Y) ^ 0xFFFFFFFF

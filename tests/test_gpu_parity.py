@@ -21,8 +21,9 @@ from seqs_amd import Engine, pack_frames, split_digests, synth  # noqa: E402
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_AUTO],
-                ids=["one_pass", "mixed", "auto"])
+@pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_WIDE,
+                                        Engine.KERNEL_AUTO],
+                ids=["one_pass", "mixed", "wide", "auto"])
 def engine(request):
     # every case through both kernel variants (and the automatic choice between them)
     if not torch.cuda.is_available():
