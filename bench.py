@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--min-warm", type=int, default=500,
                    help="device pre-warm: when --warmup is below this, (min-warm - warmup) extra untimed "
                         "launches run first, on the main stream, without the gather (reported as prewarm_launches)")
+    p.add_argument("--kernel", type=int, default=0,
+                   help="fs_ctx_set_kernel variant: 0 automatic (the 16-lane kernel), 1 / 2 the 4-lane one-pass / "
+                        "mixed-length kernels, 3 the 16-lane kernel")
     p.add_argument("--streams", type=int, default=4,
                    help="HIP streams the steps rotate over: step i+1's kernel starts on the CUs step i's "
                         "tail frees (every batch is still fully digested)")
@@ -197,6 +200,7 @@ def main():
         return main_c4(args, world, rank, local, dev)
     n = args.frames or 65536
     engine = Engine(local)
+    engine.set_kernel(args.kernel)
     batches = []
     for b in range(max(1, args.batches)):
         buf, off, ln = make_batch(args.config, n, seed=1 + 1000 * rank + b)

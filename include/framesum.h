@@ -219,7 +219,8 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
  * 768-byte pieces when a tile of 16 frames mixes very different lengths. By
  * default (variant 0) every launch reports whether its batch had such tiles and
  * the next launch picks accordingly. 1 forces the one-pass kernel, 2 the mixed
- * one. Results are identical in every case; only the speed differs. */
+ * one, 3 the 16-lane kernel (256-byte rows per frame). Results
+ * are identical in every case; only the speed differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
 /* Pinned host memory helpers for fs_digest_batch_host callers. */

@@ -35,10 +35,11 @@ static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout
 
 void build_tables(FsTables* t);
 
-// The 16-lane kernel's tables (digest_kernel_w): a frame streams as 16 lanes x 4 dword streams
-// at a 256-byte stride, so region A holds Z_256; the combine's lane shifts use Z_16..Z_48
-// (within a quad of lanes) and Z_64..Z_192 (across the 4 quads of a frame's lanes). LDS image:
-// the 13 plain [4][256] tables (copied by LDS-DMA) then region A (built in place from the basis).
+// The 16-lane kernel's tables (digest_kernel_w): a frame streams as 16 lanes, each folding its
+// 4 dwords of every 256-byte row into one accumulator, A <- Z4(Z4(Z4(Z244(A) ^ w0) ^ w1) ^ w2) ^ w3;
+// region A holds Z_244 and Z_4 (8 copies each, conflict-free). The combine's lane shifts use
+// Z_16..Z_48 (within a quad of lanes) and Z_64..Z_192 (across the 4 quads). LDS image: the 11
+// plain [4][256] tables (copied by LDS-DMA) then region A (built in place from the bases).
 struct FsTablesW {
     uint32_t z16[4][256];
     uint32_t z32[4][256];
@@ -46,18 +47,16 @@ struct FsTablesW {
     uint32_t z64[4][256];
     uint32_t z128[4][256];
     uint32_t z192[4][256];
-    uint32_t z12[4][256];
-    uint32_t z8[4][256];
     uint32_t zfin[4][4][256];  // Z_4, Z_3, Z_2, Z_1 (zfin[t] = Z_(4-t))
     uint32_t z1024[4][256];    // TX fill: long CRC corrections
-    uint32_t region_a[256][64];  // Z_256 [entry][table*8+copy], slots 32..63 unused
+    uint32_t region_a[256][64];  // [entry][op*32 + table*8 + copy], op 0 = Z_244, op 1 = Z_4
     // --- not part of the LDS image ---
-    uint32_t z256_basis[4][8];
+    uint32_t basis[2][4][8];   // op, byte table, bit: region A's entries are XORs of these
 };
-constexpr uint32_t kTablesWPlainBytes = 13u * 4096u;
+constexpr uint32_t kTablesWPlainBytes = 11u * 4096u;
 constexpr uint32_t kTablesWLdsBytes = kTablesWPlainBytes + 65536u;
 static_assert(offsetof(FsTablesW, region_a) == kTablesWPlainBytes, "FsTablesW layout");
-static_assert(offsetof(FsTablesW, z256_basis) == kTablesWLdsBytes, "FsTablesW layout");
+static_assert(offsetof(FsTablesW, basis) == kTablesWLdsBytes, "FsTablesW layout");
 
 void build_tables_w(FsTablesW* t);
 
@@ -71,9 +70,8 @@ void build_tables_w(FsTablesW* t);
 // checksums written into the frames and/or the FCS appended after them); or the RX digest of
 // wire frames whose lengths include a trailing FCS.
 enum class FsOp { kDigest, kFill, kFcs };
-// `tables_w`: the 16-lane kernel's tables. force: 0 = automatic (the 16-lane kernel), 1 / 2 = the
-// 4-lane one-pass / mixed-length kernels (the report mechanism above picks between them),
-// 3 = the 16-lane kernel.
+// `tables_w`: the 16-lane kernel's tables; force 3 = the 16-lane kernel (an experimental variant,
+// parity-tested like the others; slower than the 4-lane kernels on the benchmark configs).
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
                          int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force = 0,

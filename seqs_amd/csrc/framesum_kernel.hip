@@ -128,10 +128,10 @@ constexpr uint32_t kPlainChunk0 = 65536 / 1024;                     // first 1-K
 constexpr uint32_t kPlainChunks = kLdsRegionA / 1024;               // 40 pieces, to LDS [0, 40 KB)
 constexpr uint32_t kDmaPerWave = (kPlainChunks + kWavesPerBlock - 1) / kWavesPerBlock;
 
-// ---- LDS map of the 16-lane kernel (digest_kernel_w, below): the 13 plain tables of FsTablesW,
-// region A (Z_256), 16 x 1-KB header slots (16 frame dwords per frame), 16 x per-wave scratch.
+// ---- LDS map of the 16-lane kernel (digest_kernel_w, below): the 11 plain tables of FsTablesW,
+// region A (Z_244 and Z_4), 16 x 1-KB header slots (16 frame dwords per frame), 16 x per-wave scratch.
 constexpr uint32_t kW_Z16 = 0, kW_Z32 = 4096, kW_Z48 = 8192, kW_Z64 = 12288, kW_Z128 = 16384, kW_Z192 = 20480;
-constexpr uint32_t kW_Z12 = 24576, kW_Z8 = 28672, kW_Zfin = 32768, kW_Z1024 = 49152;
+constexpr uint32_t kW_Zfin = 24576, kW_Z1024 = 40960;
 constexpr uint32_t kW_RegionA = kTablesWPlainBytes;
 constexpr int kHdrDwW = 16;
 constexpr uint32_t kHdrWaveW = 4u * kHdrDwW * kFramesPerTile;  // 1 KB
@@ -1559,6 +1559,9 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 #ifndef FS_PREFETCH_W
 #define FS_PREFETCH_W 3
 #endif
+#ifndef FS_DIAG_W
+#define FS_DIAG_W 0  // diagnostic builds only (wrong results): 1 no combine, 2 no parse, 4 no finish, 8 masked rows lean
+#endif
 #ifdef FS_DIAG_W_DUMP
 __device__ uint32_t g_wdump[kTablesWLdsBytes / 4];
 #endif
@@ -1567,18 +1570,14 @@ constexpr int kRowDwW = 64;  // 256-byte rows
 
 __device__ __forceinline__ uint32_t zshift_w(const char* lds, uint32_t v, uint32_t k) {
     for (; k >= 1024u; k -= 1024u) v = zplain(lds, v, kW_Z1024);
-    for (; k >= 256u; k -= 256u)
-        v = lds32(lds, kW_RegionA + ((v & 0xffu) << 8)) ^ lds32(lds, kW_RegionA + (((v >> 8) & 0xffu) << 8) + 32u) ^
-            lds32(lds, kW_RegionA + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kW_RegionA + ((v >> 24) << 8) + 96u);
+    for (; k >= 256u; k -= 256u) v = zplain(lds, zplain(lds, v, kW_Z192), kW_Z64);
     if (k >= 192u) { v = zplain(lds, v, kW_Z192); k -= 192u; }
     else if (k >= 128u) { v = zplain(lds, v, kW_Z128); k -= 128u; }
     else if (k >= 64u) { v = zplain(lds, v, kW_Z64); k -= 64u; }
     if (k >= 48u) { v = zplain(lds, v, kW_Z48); k -= 48u; }
     else if (k >= 32u) { v = zplain(lds, v, kW_Z32); k -= 32u; }
     else if (k >= 16u) { v = zplain(lds, v, kW_Z16); k -= 16u; }
-    if (k >= 12u) { v = zplain(lds, v, kW_Z12); k -= 12u; }
-    else if (k >= 8u) { v = zplain(lds, v, kW_Z8); k -= 8u; }
-    else if (k >= 4u) { v = zplain(lds, v, kW_Zfin); k -= 4u; }
+    for (; k >= 4u; k -= 4u) v = zplain(lds, v, kW_Zfin);
     if (k > 0u) v = zplain(lds, v, kW_Zfin + 4096u * (4u - k));
     return v;
 }
@@ -1588,39 +1587,87 @@ struct LayoutW {
     __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift_w(lds, v, k); }
 };
 
-// Region A (Z_256, 8 copies per byte table) in place: thread t writes the 16-B chunk t & 7 of
-// entry rows t >> 3 and 128 + (t >> 3); the 8 lanes of a ds_write_b128 lane group fill one
-// entry row's 128 bytes, so the stores are bank-conflict-free. The basis (32 dwords) comes in
-// by two scalar loads; each lane selects its byte table's 8 columns.
-__device__ __forceinline__ void build_region_w(const FsTablesW* __restrict__ tabs, char* lds) {
-    typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+// Region A in place: entry row e (256 B) = [op*32 + table*8 + copy], op 0 = Z_244, op 1 = Z_4.
+// Thread t writes the 16-B chunk c = t & 15 (op c >> 3, table (c >> 1) & 3) of the rows t >> 4,
+// 64 + (t >> 4), 128 + (t >> 4) and 192 + (t >> 4): the 8 lanes of a ds_write_b128 lane group
+// fill 128 contiguous bytes, so the stores are bank-conflict-free. Each lane loads its table's
+// 8 basis columns (32 B, an L2 hit) with two dwordx4 loads issued before the descriptor and
+// table DMAs; `younger` = the VMEM instructions issued after them (waited for by the caller).
+__device__ __forceinline__ void basis_load_w(const FsTablesW* __restrict__ tabs, u32x4& b0, u32x4& b1) {
+    const uint32_t c = threadIdx.x & 15u;
+    const uint32_t* src = &tabs->basis[c >> 3][(c >> 1) & 3u][0];
+    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:16"
+                 : "=v"(b0), "=v"(b1)
+                 : "v"(src));
+}
+template <int kYounger>
+__device__ __forceinline__ void build_region_w(char* lds, u32x4 b0, u32x4 b1) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(b0), "+v"(b1) : "n"(kYounger));
     const uint32_t t = threadIdx.x;
-    const uint32_t c = t & 7u, b = c >> 1, e = t >> 3;
-    const uint64_t a = reinterpret_cast<uint64_t>(&tabs->z256_basis[0][0]);
-    const uint64_t sa = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
-    u32x16 lo, hi;
-    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(lo), "=s"(hi)
-                 : "s"(sa));
-    // branch-free selection of the byte table's columns (a select chain on the lane's table
-    // index was lowered to divergent control flow that picked wrong SGPRs for table 3)
-    const uint32_t m1 = 0u - (b & 1u), m2 = 0u - ((b >> 1) & 1u);
-    uint32_t v = 0, col7 = 0;
+    const uint32_t c = t & 15u, e = t >> 4;
+    const uint32_t col[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    uint32_t v = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t a0 = (lo[j] & ~m1) | (lo[8 + j] & m1);
-        const uint32_t a1 = (hi[j] & ~m1) | (hi[8 + j] & m1);
-        const uint32_t cj = (a0 & ~m2) | (a1 & m2);
-        if (j < 7) v ^= cj & (0u - ((e >> j) & 1u));
-        else col7 = cj;
-    }
-    *reinterpret_cast<u32x4*>(lds + kW_RegionA + e * 256u + 16u * c) = u32x4{v, v, v, v};
-    const uint32_t v2 = v ^ col7;
-    *reinterpret_cast<u32x4*>(lds + kW_RegionA + (e + 128u) * 256u + 16u * c) = u32x4{v2, v2, v2, v2};
+    for (uint32_t j = 0; j < 6; ++j) v ^= col[j] & (0u - ((e >> j) & 1u));
+    char* base = lds + kW_RegionA + e * 256u + 16u * c;
+    *reinterpret_cast<u32x4*>(base) = u32x4{v, v, v, v};
+    const uint32_t v1 = v ^ col[6], v2 = v ^ col[7], v3 = v1 ^ col[7];
+    *reinterpret_cast<u32x4*>(base + 64u * 256u) = u32x4{v1, v1, v1, v1};
+    *reinterpret_cast<u32x4*>(base + 128u * 256u) = u32x4{v2, v2, v2, v2};
+    *reinterpret_cast<u32x4*>(base + 192u * 256u) = u32x4{v3, v3, v3, v3};
 }
 
-// The plain tables (52 KB): 4 1-KB LDS-DMA pieces per wave.
+// Z(a) ^ w from region A for the operator whose slot bytes `cvec` holds (Z_244 or Z_4).
+__device__ __forceinline__ uint32_t zrep_w(const char* lds, uint32_t a, uint32_t cvec, const uint32_t (&sel)[4],
+                                           uint32_t w) {
+    const uint32_t t0 = lds32(lds, kW_RegionA + __builtin_amdgcn_perm(a, cvec, sel[0]));
+    const uint32_t t1 = lds32(lds, kW_RegionA + __builtin_amdgcn_perm(a, cvec, sel[1]));
+    const uint32_t t2 = lds32(lds, kW_RegionA + __builtin_amdgcn_perm(a, cvec, sel[2]));
+    const uint32_t t3 = lds32(lds, kW_RegionA + __builtin_amdgcn_perm(a, cvec, sel[3]));
+    return xor3(xor3(t0, t1, t2), t3, w);
+}
+
+struct KeysW {
+    uint32_t c244, c4;  // slot bytes of the lane's copy of each byte table, Z_244 / Z_4
+    uint32_t sel[4];    // v_perm selectors of the 4 lookups (table rotation by lane)
+};
+
+// One row of the lane: A <- Z4(Z4(Z4(Z244(A) ^ w0) ^ w1) ^ w2) ^ w3, and the 4 dwords' sums.
+__device__ __forceinline__ void lean_row_w(const char* lds, const KeysW& k, u32x4 v, uint32_t& A, uint32_t& cs) {
+    A = zrep_w(lds, A, k.c244, k.sel, v.x);
+    A = zrep_w(lds, A, k.c4, k.sel, v.y);
+    A = zrep_w(lds, A, k.c4, k.sel, v.z);
+    A = zrep_w(lds, A, k.c4, k.sel, v.w);
+    cs = sad16(v.x, cs);
+    cs = sad16(v.y, cs);
+    cs = sad16(v.z, cs);
+    cs = sad16(v.w, cs);
+}
+
+// A masked row (masked_row's masks and realignment, one accumulator).
+__device__ __forceinline__ void masked_row_w(const char* lds, const KeysW& k, u32x4 u, int rel, int p, int nd,
+                                             uint32_t sa, uint32_t tail_mask, uint32_t& A, uint32_t& cs) {
+    const uint32_t head_mask = 0xffffffffu << (8u * sa);
+    const int sh = p - rel;
+    uint32_t v[4];
+    v[0] = u.x;
+    v[1] = (sh == 0) ? u.y : u.x;
+    v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
+    v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int x = rel + j;
+        uint32_t d = (x >= 0) ? v[j] : 0u;
+        uint32_t c = 0u;
+        if (x == 0) { d &= head_mask; c = head_mask; }
+        if (x == 1) c = ~head_mask;
+        if (x == nd - 1) d &= tail_mask;
+        A = zrep_w(lds, A, j == 0 ? k.c244 : k.c4, k.sel, d ^ c);
+        cs = sad16(d, cs);
+    }
+}
+
+// The plain tables (44 KB): 3 1-KB LDS-DMA pieces per wave.
 __device__ __forceinline__ void plain_dma_w(const FsTablesW* __restrict__ tabs, const char* lds, uint32_t wave,
                                             uint32_t lane) {
     constexpr uint32_t kPieces = kTablesWPlainBytes / 1024u;
@@ -1761,12 +1808,12 @@ __device__ __forceinline__ void prefetch_w(const UnitW& U, u32x4 (&pf)[kPfW]) {
     }
 }
 
-// The 64-stream combine of a pass (16-lane mapping): U = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3 ^ junk
-// per lane, Z_(16(3 - (j & 3))) per lane and a quad XOR, Z_(64(3 - (j >> 2))) per quad and an
-// XOR over the quads (DPP row_ror 4 and 8); the checksum partials folded and summed likewise.
-__device__ __forceinline__ void combine_w(const char* lds, uint32_t j, const uint32_t (&A)[4], uint32_t cs,
-                                          uint32_t junk, uint32_t& Y, uint32_t& csum) {
-    const uint32_t U = zplain(lds, A[0], kW_Z12) ^ zplain(lds, A[1], kW_Z8) ^ zplain(lds, A[2], kW_Zfin) ^ A[3] ^ junk;
+// The 16-lane combine of a pass: A ^ junk per lane, Z_(16(3 - (j & 3))) per lane and a quad
+// XOR, Z_(64(3 - (j >> 2))) per quad and an XOR over the quads (DPP row_ror 4 and 8); the
+// checksum partials folded and summed likewise.
+__device__ __forceinline__ void combine_w(const char* lds, uint32_t j, uint32_t A, uint32_t cs, uint32_t junk,
+                                          uint32_t& Y, uint32_t& csum) {
+    const uint32_t U = A ^ junk;
     cs -= sad16(junk, 0u);
     const uint32_t w = j & 3u, q = j >> 2;
     uint32_t y = zplain(lds, U, w == 0u ? kW_Z48 : w == 1u ? kW_Z32 : kW_Z16);
@@ -1808,12 +1855,13 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     const uint32_t wb = kW_Wave + wave * kW_WaveBytes;
     const uint32_t pk = wb + kW_Park;
 
-    LaneKeys keys;
+    KeysW keys;
     {
         const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
-        keys.cvec = 0;
+        keys.c244 = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) keys.cvec |= (32u * j + 4u * c) << (8u * j);
+        for (uint32_t j = 0; j < 4; ++j) keys.c244 |= (32u * j + 4u * c) << (8u * j);
+        keys.c4 = keys.c244 + 0x80808080u;  // op 1 = slots 32..63 (+128 bytes)
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
             const uint32_t b = (k + h) & 3u;
@@ -1831,6 +1879,8 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         uint64_t S = 0;
         uint32_t len = 0;
         const bool first = st < nst;
+        u32x4 b0, b1;
+        basis_load_w(tabs, b0, b1);
         if (first) tile_descriptors(st, grp, n, offsets, lengths, S, len, fpt);
         plain_dma_w(tabs, lds, wave, lane);
 #ifdef FS_DIAG_W_DMA_A
@@ -1843,7 +1893,7 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             }
         }
 #else
-        build_region_w(tabs, lds);
+        build_region_w<3>(lds, b0, b1);  // younger: the 3 table pieces (and the 2 descriptor loads)
 #endif
         wait_tied<0>(S, len);
         if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
@@ -1889,8 +1939,9 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * grp);
             const uint64_t S = ((uint64_t)d.y << 32) | d.x;
             const bool valid = grp < fpt && st * fpt + grp < n;
-            parse_tile<kOps, kHdrDwW>(hw, grp, gl, (uint32_t)S & 3u, d.z, mtu,
-                                      reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), valid && gl == 0u, pk);
+            if (!(FS_DIAG_W & 2))
+                parse_tile<kOps, kHdrDwW>(hw, grp, gl, (uint32_t)S & 3u, d.z, mtu,
+                                          reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), valid && gl == 0u, pk);
             parsed = true;
         };
         // the next super-tile: geometry, header DMA, the descriptors of the one after, its first unit
@@ -1914,8 +1965,7 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         for (int p = 0; p < npass; ++p) {
             const uint32_t j = lane & 15u;
             const UnitW U = unit_w(lds, gb, p, lane >> 4, j, frames);
-            uint32_t A[4] = {0u, 0u, 0u, 0u};
-            uint32_t cs = 0u;
+            uint32_t A = 0u, cs = 0u;
             if (U.P > 0 && !pre) prefetch_w(U, pf);
             pre = false;
             const uint32_t tail_mask = U.tail_mask;
@@ -1927,8 +1977,8 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 for (int i = 0; i < kPfW; ++i) {
                     const int r = r0 + i;
                     const int rel = U.rel0 + kRowDwW * r;
-                    if (r < U.H) masked_row<kW_RegionA>(lds, keys, pf[i], rel, load_pos(rel, U.lo), U.nd, U.sa, tail_mask, A, cs);
-                    else lean_row<kW_RegionA>(lds, keys, pf[i], A, cs);
+                    if (r < U.H && !(FS_DIAG_W & 8)) masked_row_w(lds, keys, pf[i], rel, load_pos(rel, U.lo), U.nd, U.sa, tail_mask, A, cs);
+                    else lean_row_w(lds, keys, pf[i], A, cs);
                     if (kKind != 1 && i == kPfW - 1) lastw = pf[i].w;
                     if (kKind == 1) {
                         const int rn = rel + kRowDwW * kPfW;
@@ -1944,7 +1994,7 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 const uint32_t* pb = U.gfb + (U.rel0 + kRowDwW * (r0 + kPfW));
 #pragma unroll
                 for (int i = 0; i < kPfW; ++i) {
-                    lean_row<kW_RegionA>(lds, keys, pf[i], A, cs);
+                    lean_row_w(lds, keys, pf[i], A, cs);
                     if (kKind != 1 && i == kPfW - 1) lastw = pf[i].w;
                     if (kKind == 1) {
                         pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwW * i);
@@ -1991,12 +2041,9 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             // dword (lane 15's 4th) still holds the up to 3 bytes past the frame end
             uint32_t junk = 0u;
             if (U.P > 0 && U.H < U.P && j == 15u && U.nd > 0) junk = lastw & ~tail_mask;
-            if (U.P == 0) {
-                A[0] = A[1] = A[2] = A[3] = 0u;
-                cs = 0u;
-            }
-            uint32_t Y, csum;
-            combine_w(lds, j, A, cs, junk, Y, csum);
+            if (U.P == 0) A = cs = 0u;
+            uint32_t Y = A, csum = cs;
+            if (!(FS_DIAG_W & 1)) combine_w(lds, j, A, cs, junk, Y, csum);
             if (j == 0u) {
                 const uint32_t f = *reinterpret_cast<const uint8_t*>(lds + gb + kW_GeoOrder + 4u * (uint32_t)p + (lane >> 4));
                 *reinterpret_cast<uint2*>(lds + wb + kW_Ycs + 8u * f) = make_uint2(Y, csum);
@@ -2016,7 +2063,7 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
             const uint32_t grp = ln >> 2, gl = ln & 3u;
             const bool valid = grp < fpt && st * fpt + grp < n;
-            if (valid && gl == 0u) {
+            if (valid && gl == 0u && !(FS_DIAG_W & 4)) {
                 const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * grp);
                 const uint64_t S = ((uint64_t)d.y << 32) | d.x;
                 const uint32_t len = d.z;
@@ -2078,7 +2125,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     uint32_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     uint2* o = reinterpret_cast<uint2*>(out);
-    if ((force == 0 || force == 3) && tables_w) {
+    if (force == 3 && tables_w) {
 #define FS_LAUNCH_W(OPS)                                                                                       \
     hipLaunchKernelGGL((digest_kernel_w<OPS>), dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, \
                        mtu, tables_w, o, status, wframes, tx, fpt)

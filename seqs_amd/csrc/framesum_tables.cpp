@@ -69,28 +69,30 @@ void build_tables_w(FsTablesW* t) {
     std::memset(t, 0, sizeof(*t));
     uint32_t t1[256];
     byte_table(t1);
-    static uint32_t zrow[4][256];
-    op_table(t1, 256, zrow);
-    for (uint32_t e = 0; e < 256; ++e)
+    static uint32_t zop[2][4][256];
+    op_table(t1, 244, zop[0]);
+    op_table(t1, 4, zop[1]);
+    for (uint32_t o = 0; o < 2; ++o)
+        for (uint32_t e = 0; e < 256; ++e)
+            for (uint32_t b = 0; b < 4; ++b)
+                for (uint32_t c = 0; c < 8; ++c) t->region_a[e][32 * o + 8 * b + c] = zop[o][b][e];
+    for (uint32_t o = 0; o < 2; ++o)
         for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t c = 0; c < 8; ++c) t->region_a[e][8 * b + c] = zrow[b][e];
-    for (uint32_t b = 0; b < 4; ++b)
-        for (uint32_t j = 0; j < 8; ++j) t->z256_basis[b][j] = zrow[b][1u << j];
-    for (uint32_t b = 0; b < 4; ++b)
-        for (uint32_t e = 0; e < 256; ++e) {
-            uint32_t v = 0;
-            for (uint32_t j = 0; j < 8; ++j)
-                if ((e >> j) & 1u) v ^= t->z256_basis[b][j];
-            if (v != zrow[b][e]) throw std::logic_error("Z_256 basis mismatch");
-        }
+            for (uint32_t j = 0; j < 8; ++j) t->basis[o][b][j] = zop[o][b][1u << j];
+    for (uint32_t o = 0; o < 2; ++o)
+        for (uint32_t b = 0; b < 4; ++b)
+            for (uint32_t e = 0; e < 256; ++e) {
+                uint32_t v = 0;
+                for (uint32_t j = 0; j < 8; ++j)
+                    if ((e >> j) & 1u) v ^= t->basis[o][b][j];
+                if (v != zop[o][b][e]) throw std::logic_error("region A basis mismatch");
+            }
     op_table(t1, 16, t->z16);
     op_table(t1, 32, t->z32);
     op_table(t1, 48, t->z48);
     op_table(t1, 64, t->z64);
     op_table(t1, 128, t->z128);
     op_table(t1, 192, t->z192);
-    op_table(t1, 12, t->z12);
-    op_table(t1, 8, t->z8);
     for (int k = 0; k < 4; ++k) op_table(t1, 4 - k, t->zfin[k]);
     op_table(t1, 1024, t->z1024);
     if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");

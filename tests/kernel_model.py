@@ -204,3 +204,61 @@ def crc32_model_w(buf: bytes, S: int, length: int) -> int:
         Y ^= W if quad_level[q] is None else apply(quad_level[q], W)
     t = (4 - (E & 3)) & 3
     return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
+
+
+# ---- the 16-lane kernel with ONE stream per lane: each 256-byte row folds the lane's 4 dwords
+# into its accumulator by A <- Z4(Z4(Z4(Z244(A) ^ w0) ^ w1) ^ w2) ^ w3 (= Z256(A) ^ Z12(w0) ^
+# Z8(w1) ^ Z4(w2) ^ w3), so the combine only folds 16 lane values per frame.
+Z244 = op_table(244)
+
+
+def crc32_model_w1(buf: bytes, S: int, length: int) -> int:
+    E = S + length
+    if length < 4:
+        return crc32_model(buf, S, length)
+    sdw = S >> 2
+    nd = ((E + 3) >> 2) - sdw
+    sa = S & 3
+    te = (E & 3) or 4
+    head_mask = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
+    tail_mask = 0xFFFFFFFF if te == 4 else (1 << (8 * te)) - 1
+    padded = bytes(buf) + b"\0" * 8
+
+    def dword(rel):
+        return struct.unpack_from("<I", padded, 4 * (sdw + rel))[0]
+
+    R = (nd + 63) // 64
+    A = [0] * 16
+    for r in range(R):
+        for lane in range(16):
+            rel = nd - 64 * R + 64 * r + 4 * lane
+            d = []
+            for j in range(4):
+                rj = rel + j
+                dc = 0
+                if rj >= 0:
+                    mk, x = 0xFFFFFFFF, 0
+                    if rj == 0:
+                        mk &= head_mask
+                        x ^= head_mask
+                    if rj == 1:
+                        x ^= (~head_mask) & 0xFFFFFFFF
+                    if rj == nd - 1:
+                        mk &= tail_mask
+                    dc = (dword(rj) & mk) ^ x
+                d.append(dc)
+            a = apply(Z244, A[lane]) ^ d[0]
+            a = apply(Z4, a) ^ d[1]
+            a = apply(Z4, a) ^ d[2]
+            A[lane] = apply(Z4, a) ^ d[3]
+    quad_tab = [Z48, Z32, Z16, None]
+    quad_level = [Z192, Z128, Z64Q, None]
+    Y = 0
+    for q in range(4):
+        W = 0
+        for w in range(4):
+            u = A[4 * q + w]
+            W ^= u if quad_tab[w] is None else apply(quad_tab[w], u)
+        Y ^= W if quad_level[q] is None else apply(quad_level[q], W)
+    t = (4 - (E & 3)) & 3
+    return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
