@@ -345,7 +345,7 @@ __device__ __forceinline__ uint32_t slot_sum(const char* lds, uint32_t hw, uint3
 }
 
 // exact sum of frame bytes [p0, p1) straight from global memory (rare paths)
-__device__ uint32_t global_sum(const uint32_t* fb, uint32_t sa, int p0, int p1) {
+__device__ __forceinline__ uint32_t global_sum(const uint32_t* fb, uint32_t sa, int p0, int p1) {
     uint32_t s = 0;
     if (p1 <= p0) return s;
     const int a0 = (int)sa + p0, a1 = (int)sa + p1;
@@ -493,9 +493,11 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, ui
 // (the bytes [0, off) of the Ethernet + IP headers; the Ethernet padding [end, len) when it
 // lies in the slot), then the parser lane's gates and corrections, parked in LDS.
 // `pk`: where the parse result is parked (the 4-lane kernels park it in the header slot itself).
+// parse_tile_body: the same, inlined (the 16-lane kernel's single parse site: a call there would
+// end in a vmcnt(0) that drains the row ring).
 template <uint32_t kOps, int kSlotDw = kHdrDwords>
-__device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
-                                                     uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk) {
+__device__ __forceinline__ void parse_tile_body(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
+                                                uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk) {
     const char* lds = g_lds;
     const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3));
     const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
@@ -514,9 +516,14 @@ __device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, 
     }
     if (parser) park_parsed<kOps>(g_lds, pk, grp, parse_frame<kOps, kSlotDw>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
 }
+template <uint32_t kOps, int kSlotDw = kHdrDwords>
+__device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
+                                                     uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk) {
+    parse_tile_body<kOps, kSlotDw>(hw, grp, gl, sa, len, mtu, fbs, parser, pk);
+}
 
 // Final L4 checksum + verdict (parser lane) once the streamed sum is known.
-__device__ uint32_t finish_l4(const uint32_t* fb, uint32_t sa, uint32_t len, const Parsed& P, uint64_t main_sum,
+__device__ __forceinline__ uint32_t finish_l4(const uint32_t* fb, uint32_t sa, uint32_t len, const Parsed& P, uint64_t main_sum,
                               uint32_t& verdict) {
     // Every term is congruent (mod 65535) to its exact native contribution, and the true
     // total is > 0 (the pseudo-header protocol word is 6 or 17), so adding 65535 * 2^20
@@ -1557,7 +1564,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 // last block.
 
 #ifndef FS_PREFETCH_W
-#define FS_PREFETCH_W 3
+#define FS_PREFETCH_W 6
 #endif
 #ifndef FS_DIAG_W
 #define FS_DIAG_W 0  // diagnostic builds only (wrong results): 1 no combine, 2 no parse, 4 no finish, 8 masked rows lean
@@ -1927,24 +1934,23 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     while (st < nst) {
         const int npass = (int)__builtin_amdgcn_readfirstlane(lds32(lds, gb + kW_GeoNpass));
         const uint32_t gnext = gb == wb + kW_Geo ? wb + kW_Geo + kW_GeoBytes : wb + kW_Geo;  // the other buffer
-        bool parsed = false, next_ready = false;
-        // header parse of the whole super-tile (4-lane mapping), once the header DMA has landed:
-        // it was issued before this super-tile's first rows
-        auto parse = [&](bool refilled) {
-            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfW);
+        // ---- header parse of the whole super-tile (4-lane mapping), inlined, before its rows: the
+        // header DMA was issued before the ring's kPfW loads of its first rows (or before everything)
+        {
+            if (pre) __builtin_amdgcn_s_waitcnt(0x0070 | kPfW);
             else __builtin_amdgcn_s_waitcnt(0x0070);
-            uint32_t ln;
-            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-            const uint32_t grp = ln >> 2, gl = ln & 3u;
+            const uint32_t grp = lane >> 2, gl = lane & 3u;
             const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * grp);
             const uint64_t S = ((uint64_t)d.y << 32) | d.x;
             const bool valid = grp < fpt && st * fpt + grp < n;
             if (!(FS_DIAG_W & 2))
-                parse_tile<kOps, kHdrDwW>(hw, grp, gl, (uint32_t)S & 3u, d.z, mtu,
-                                          reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), valid && gl == 0u, pk);
-            parsed = true;
-        };
-        // the next super-tile: geometry, header DMA, the descriptors of the one after, its first unit
+                parse_tile_body<kOps, kHdrDwW>(hw, grp, gl, (uint32_t)S & 3u, d.z, mtu,
+                                               reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
+                                               valid && gl == 0u, pk);
+        }
+        bool next_ready = false;
+        // the next super-tile: geometry, header DMA (the slot is free: parsed above), the
+        // descriptors of the one after, its first unit
         auto setup_next = [&](bool in_block) -> UnitW {
             // the descriptor DMA is older than the ring's kPfW youngest loads (or than everything)
             if (in_block) __builtin_amdgcn_s_waitcnt(0x0070 | kPfW);
@@ -1968,88 +1974,57 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             uint32_t A = 0u, cs = 0u;
             if (U.P > 0 && !pre) prefetch_w(U, pf);
             pre = false;
-            const uint32_t tail_mask = U.tail_mask;
-            // general block: rows below H masked; refill 0 none, 1 this unit, 2 the next unit
-            uint32_t lastw = 0u;  // the pass's last row's last dword, kept before its slot is refilled
-            auto block = [&](int r0, const UnitW& Un, auto kind_tag) {
-                constexpr int kKind = decltype(kind_tag)::value;
+            // the pass's last dword (lane 15's 4th of the last row) holds up to 3 bytes past
+            // the frame end: masked in the last block (a masked last row masks it itself)
+            const uint32_t endmask = (j == 15u && U.nd > 0 && U.H < U.P) ? U.tail_mask : 0xffffffffu;
+            for (int r0 = 0; r0 < U.P; r0 += kPfW) {
+                const bool lastb = r0 + kPfW == U.P;
+                // the refills: this unit's rows kPfW ahead, or (last block) the next unit's first
+                // rows -- the next pass's, the next super-tile's, or (none left) this unit's own
+                // first rows again (harmless cache hits): ONE load per ring slot on every path, so
+                // the compiler never copies an in-flight register
+                const uint32_t* rb = U.gfb;  // refill rows: frame base, first row's dword, clamp floor,
+                int rrel = U.rel0 + kRowDwW * (r0 + kPfW), rlo = U.lo, rH = U.H - (r0 + kPfW);  // clamped rows
+                if (lastb) {
+                    UnitW Nx;
+                    Nx.P = 0;
+                    if (p + 1 < npass) Nx = unit_w(lds, gb, p + 1, lane >> 4, j, frames);
+                    else if (st + nwaves < nst) Nx = setup_next(true);
+                    pre = Nx.P > 0;
+                    if (!pre) Nx = U;
+                    rb = Nx.gfb;
+                    rrel = Nx.rel0;
+                    rlo = Nx.lo;
+                    rH = Nx.H;
+                }
+                const uint32_t* pb = rb + rrel;
 #pragma unroll
                 for (int i = 0; i < kPfW; ++i) {
                     const int r = r0 + i;
                     const int rel = U.rel0 + kRowDwW * r;
-                    if (r < U.H && !(FS_DIAG_W & 8)) masked_row_w(lds, keys, pf[i], rel, load_pos(rel, U.lo), U.nd, U.sa, tail_mask, A, cs);
-                    else lean_row_w(lds, keys, pf[i], A, cs);
-                    if (kKind != 1 && i == kPfW - 1) lastw = pf[i].w;
-                    if (kKind == 1) {
-                        const int rn = rel + kRowDwW * kPfW;
-                        pf[i] = load_row(U.gfb, r + kPfW < U.H ? load_pos(rn, U.lo) : rn);
-                    } else if (kKind == 2) {
-                        const int rn = Un.rel0 + kRowDwW * i;
-                        pf[i] = load_row(Un.gfb, i < Un.H ? load_pos(rn, Un.lo) : rn);
+                    if (r < U.H && !(FS_DIAG_W & 8)) {
+                        masked_row_w(lds, keys, pf[i], rel, load_pos(rel, U.lo), U.nd, U.sa, U.tail_mask, A, cs);
+                    } else if (i == kPfW - 1) {
+                        u32x4 v = pf[i];
+                        v.w &= lastb ? endmask : 0xffffffffu;
+                        lean_row_w(lds, keys, v, A, cs);
+                    } else {
+                        lean_row_w(lds, keys, pf[i], A, cs);
                     }
-                }
-            };
-            auto lean_block = [&](int r0, const UnitW& Un, auto kind_tag) {
-                constexpr int kKind = decltype(kind_tag)::value;
-                const uint32_t* pb = U.gfb + (U.rel0 + kRowDwW * (r0 + kPfW));
-#pragma unroll
-                for (int i = 0; i < kPfW; ++i) {
-                    lean_row_w(lds, keys, pf[i], A, cs);
-                    if (kKind != 1 && i == kPfW - 1) lastw = pf[i].w;
-                    if (kKind == 1) {
-                        pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwW * i);
-                    } else if (kKind == 2) {
-                        const int rn = Un.rel0 + kRowDwW * i;
-                        pf[i] = load_row(Un.gfb, i < Un.H ? load_pos(rn, Un.lo) : rn);
-                    }
+                    if (i < rH) pf[i] = load_row(rb, load_pos(rrel + kRowDwW * i, rlo));  // wave-uniform branch
+                    else pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwW * i);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-            };
-            using K0 = std::integral_constant<int, 0>;
-            using K1 = std::integral_constant<int, 1>;
-            using K2 = std::integral_constant<int, 2>;
-            for (int r0 = 0; r0 < U.P; r0 += kPfW) {
-                const bool lastb = r0 + kPfW == U.P;
-                if (!lastb) {
-                    if (r0 >= U.H) lean_block(r0, U, K1());
-                    else block(r0, U, K1());
-                    if (!parsed) parse(true);
-                    continue;
-                }
-                // the last block of the pass refills the ring with the next unit's first rows
-                UnitW Un;
-                Un.P = 0;
-                if (p + 1 < npass) {
-                    Un = unit_w(lds, gb, p + 1, lane >> 4, j, frames);
-                } else if (st + nwaves < nst) {
-                    // the next super-tile's header DMA rewrites the slot: parse this one first
-                    if (!parsed) parse(false);
-                    Un = setup_next(true);
-                }
-                if (Un.P > 0) {
-                    pre = true;
-                    if (r0 >= U.H) lean_block(r0, Un, K2());
-                    else block(r0, Un, K2());
-                    if (!parsed) parse(true);
-                } else {
-                    if (r0 >= U.H) lean_block(r0, Un, K0());
-                    else block(r0, Un, K0());
-                    if (!parsed) parse(false);
-                }
             }
-            // combine the pass: the last row was lean unless every row was masked; its last
-            // dword (lane 15's 4th) still holds the up to 3 bytes past the frame end
-            uint32_t junk = 0u;
-            if (U.P > 0 && U.H < U.P && j == 15u && U.nd > 0) junk = lastw & ~tail_mask;
+            // combine the pass
             if (U.P == 0) A = cs = 0u;
             uint32_t Y = A, csum = cs;
-            if (!(FS_DIAG_W & 1)) combine_w(lds, j, A, cs, junk, Y, csum);
+            if (!(FS_DIAG_W & 1)) combine_w(lds, j, A, cs, 0u, Y, csum);
             if (j == 0u) {
                 const uint32_t f = *reinterpret_cast<const uint8_t*>(lds + gb + kW_GeoOrder + 4u * (uint32_t)p + (lane >> 4));
                 *reinterpret_cast<uint2*>(lds + wb + kW_Ycs + 8u * f) = make_uint2(Y, csum);
             }
         }
-        if (!parsed) parse(false);
         if (!next_ready && st + nwaves < nst) {
             const UnitW Un = setup_next(false);
             if (Un.P > 0) {
