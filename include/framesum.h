@@ -101,9 +101,9 @@ const char* fs_last_error(const fs_ctx* ctx);
 
 /* Batched digest, device-resident. All pointers are DEVICE pointers.
  *   frame i = frames[offsets[i] : offsets[i] + lengths[i]]  (any byte alignment,
- *   frames may overlap or be sparse; the engine may read up to 3 bytes past a
- *   frame's end, i.e. `frames` must be readable up to round_up(end, 4), and up
- *   to 12 bytes before a frame's start, but never before frames[0]).
+ *   frames may overlap or be sparse; the engine reads whole 64-byte-aligned
+ *   blocks that hold frame bytes -- up to 63 bytes around a frame, never outside
+ *   the memory pages that hold its bytes -- and ignores the bytes outside it).
  *   out[i] receives the digest; status (nullable) receives the fs_verdict.
  * Asynchronous on `stream` (a hipStream_t; NULL = the null stream). */
 fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths,
@@ -218,9 +218,11 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
  * for batches of similar frame lengths, and one that splits long frames into
  * 768-byte pieces when a tile of 16 frames mixes very different lengths. By
  * default (variant 0) every launch reports whether its batch had such tiles and
- * the next launch picks accordingly. 1 forces the one-pass kernel, 2 the mixed
- * one, 3 the 16-lane kernel (256-byte rows per frame). Results
- * are identical in every case; only the speed differs. */
+ * the next launch picks accordingly (the one-pass choice reads each frame as the
+ * 64-byte blocks that hold it). 1 forces the one-pass kernel with rows anchored at
+ * the frame end, 2 the mixed one, 3 the 16-lane kernel (256-byte rows per frame;
+ * DESIGN.md §3.8), 4 the one-pass kernel with block-aligned rows. Results are
+ * identical in every case; only the speed differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
 /* Pinned host memory helpers for fs_digest_batch_host callers. */

@@ -70,6 +70,8 @@ void build_tables_w(FsTablesW* t);
 // checksums written into the frames and/or the FCS appended after them); or the RX digest of
 // wire frames whose lengths include a trailing FCS.
 enum class FsOp { kDigest, kFill, kFcs };
+// force 4 = the one-pass kernel with block-aligned rows (what force 0 uses for the one-pass choice;
+// force 1 keeps the end-anchored rows).
 // `tables_w`: the 16-lane kernel's tables; force 3 = the 16-lane kernel (an experimental variant,
 // parity-tested like the others; slower than the 4-lane kernels on the benchmark configs).
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,

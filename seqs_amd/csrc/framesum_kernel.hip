@@ -89,6 +89,14 @@ constexpr int kPrefetch = FS_PREFETCH;  // the mixed-length kernel's ring (a div
 #define FS_PREFETCH_A 6
 #endif
 constexpr int kPrefetchA = FS_PREFETCH_A;  // the one-pass kernel's ring
+#ifndef FS_PREFETCH_AL
+#define FS_PREFETCH_AL 5
+#endif
+// ... with block-aligned rows: an MTU frame (1500 B) spans 24 or 25 blocks, so a tile's rows
+// are a multiple of 5 with no padding row
+constexpr int kPrefetchAl = FS_PREFETCH_AL;
+template <bool kAl>
+constexpr int kRingA = kAl ? kPrefetchAl : kPrefetchA;
 
 // Header slots: frame dwords [0, 32) of each group's frame, written by 8 dword LDS-DMA
 // instructions per wave in the layout [x >> 2][group][x & 3] (256 B per instruction),
@@ -301,6 +309,43 @@ __device__ __forceinline__ void masked_row(const char* lds, const LaneKeys& k, u
         if (x == nd - 1) d &= tail_mask;
         A[j] = zrep<kRegion>(lds, A[j], k, d ^ c);
         cs = sad16(d, cs);
+    }
+}
+
+// Block-aligned rows (digest_kernel_a<kOps, true>): a chunk is always loaded where it lies (or,
+// wholly before the frame, somewhere irrelevant), so no realignment. Dwords at or past the frame
+// end (only in the last row) leave the stream untouched: the combine then shifts that stream
+// by its distance to the frame end, which the skipped update would have overshot.
+__device__ __forceinline__ void masked_row_al(const char* lds, const LaneKeys& k, u32x4 u, int rel, int nd,
+                                              uint32_t sa, uint32_t tail_mask, uint32_t (&A)[4], uint32_t& cs) {
+    const uint32_t head_mask = 0xffffffffu << (8u * sa);
+    const uint32_t v[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int x = rel + j;
+        uint32_t d = (x >= 0) ? v[j] : 0u;
+        uint32_t c = 0u;
+        if (x == 0) { d &= head_mask; c = head_mask; }
+        if (x == 1) c = ~head_mask;
+        if (x == nd - 1) d &= tail_mask;
+        const bool in = x < nd;
+        const uint32_t a = zrep(lds, A[j], k, d ^ c);
+        A[j] = in ? a : A[j];
+        cs = sad16(in ? d : 0u, cs);
+    }
+}
+// The last row of block-aligned rows when it is otherwise lean.
+__device__ __forceinline__ void tail_row_al(const char* lds, const LaneKeys& k, u32x4 u, int rel, int nd,
+                                            uint32_t tail_mask, uint32_t (&A)[4], uint32_t& cs) {
+    const uint32_t v[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int x = rel + j;
+        const uint32_t d = (x == nd - 1) ? (v[j] & tail_mask) : v[j];
+        const bool in = x < nd;
+        const uint32_t a = zrep(lds, A[j], k, d);
+        A[j] = in ? a : A[j];
+        cs = sad16(in ? d : 0u, cs);
     }
 }
 
@@ -865,8 +910,11 @@ struct TileA {
     int lo;     // lowest frame dword a clamped row load may start at
     int P;      // wave-uniform: rows of the tile (a multiple of kPrefetch; 0 = no rows)
     int H;      // wave-uniform: leading rows that take the masked path
+    uint32_t ph;  // block-aligned rows: absolute 64-B block phase (in dwords) of frame dword 0
     // derived per use (they would otherwise hold VGPRs across the row loop)
     __device__ __forceinline__ uint32_t sa() const { return (uint32_t)S & 3u; }
+    // block-aligned rows: dwords past the frame end in its last row (the row ends on a 64-B block)
+    __device__ __forceinline__ int ealign() const { return (16 - (int)((ph + (uint32_t)nd()) & 15u)) & 15; }
     __device__ __forceinline__ uint64_t sdw() const { return S >> 2; }
     // dwords the frame touches (incl. frames under 4 bytes)
     __device__ __forceinline__ int ndall() const { return (int)((sa() + len + 3u) >> 2); }
@@ -882,26 +930,36 @@ struct TileA {
     }
 };
 
+// kAl: BLOCK-ALIGNED rows -- each frame's rows are the 64-B blocks (half 128-B lines) that hold
+// it, the last one ending on the block boundary after the frame end (nd + ealign() dwords from
+// frame dword 0), so a row load never straddles a line; the end-anchored rows otherwise
+// (ending at the frame's dword-rounded end).
+template <bool kAl>
 __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
                                               uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
                                               uint32_t fpt) {
     T.len = (grp < fpt && tile * fpt + grp < n) ? len : 0u;
     T.S = S;
+    T.ph = (uint32_t)((reinterpret_cast<uint64_t>(frames) >> 2) + T.sdw()) & 15u;
     const int nd = T.nd();
-    const int rows = (nd + kRowDwords - 1) / kRowDwords;
+    const int ndb = (kAl && nd > 0) ? nd + T.ealign() : nd;  // stream dwords up to the last row's end
+    const int rows = kAl ? (int)((T.ph + (uint32_t)ndb) >> 4) * (nd > 0) : (nd + kRowDwords - 1) / kRowDwords;
     const int R = group_max(rows);
-    T.P = (R + kPrefetchA - 1) / kPrefetchA * kPrefetchA;
+    T.P = (R + kRingA<kAl> - 1) / kRingA<kAl> * kRingA<kAl>;
     uint64_t ld_sdw = T.sdw();
-    int ld_nd = nd;
+    int ld_nd = ndb;
+    uint32_t ld_ph = T.ph;
     {
         const uint64_t ball = __ballot(rows == R);  // never 0: some lane holds the maximum
         const int src = (int)__builtin_ctzll(ball);
         const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ld_sdw, src);
         const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ld_sdw >> 32), src);
-        const int s_nd = __builtin_amdgcn_readlane(nd, src);
+        const int s_nd = __builtin_amdgcn_readlane(ndb, src);
+        const uint32_t s_ph = (uint32_t)__builtin_amdgcn_readlane((int)ld_ph, src);
         if (nd == 0) {
             ld_sdw = ((uint64_t)s_hi << 32) | s_lo;
             ld_nd = s_nd;
+            ld_ph = s_ph;
         }
     }
     T.gfb = reinterpret_cast<const uint32_t*>(frames + (ld_sdw << 2));
@@ -910,11 +968,14 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     // chunk for frames under 4 dwords), so lanes idling through a tile's longest frame re-read
     // one cached line instead of fetching the bytes that precede their frame; a chunk that
     // straddles the frame start is loaded where it lies unless that is below frames[0].
-    T.lo = max(ld_sdw > (1u << 24) ? -(1 << 24) : -(int)ld_sdw, min(0, ld_nd - 4));
+    // Block-aligned rows: lo = the frame dword where the frame's first block starts; a chunk
+    // below it reloads the lane's chunk of that block (a row inside a block that holds a frame
+    // byte never leaves that byte's page, so it needs no other clamp).
+    T.lo = kAl ? -(int)ld_ph : max(ld_sdw > (1u << 24) ? -(1 << 24) : -(int)ld_sdw, min(0, ld_nd - 4));
     // Masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
     // dword before the frame. The group's lane 0 has the lowest rel: row r is lean for the
     // group once nd - 16 P + 16 r >= 2.
-    const int need = 2 - (nd - kRowDwords * T.P);
+    const int need = 2 - (ndb - kRowDwords * T.P);
     const int h = (nd > 0 && need > 0) ? (need + kRowDwords - 1) / kRowDwords : 0;
     T.H = min(group_max(h), T.P);
 }
@@ -1094,12 +1155,13 @@ __device__ __forceinline__ uint32_t first_tile(uint32_t wave) {
     return blockIdx.x * kWavesPerBlock + wave;
 }
 
-template <uint32_t kOps>
+template <uint32_t kOps, bool kAl>
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
                 const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx, uint32_t fpt) {
     char* lds = g_lds;
+    constexpr int kPfA = kRingA<kAl>;
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
@@ -1112,6 +1174,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     fpt = __builtin_amdgcn_readfirstlane(fpt);
     const uint32_t ntiles = (n + fpt - 1) / fpt;
     const uint32_t hw = kLdsHdr + wave * kHdrWaveBytes;  // this wave's header slots
+    // where a masked row's chunk is loaded (block-aligned rows: where it lies, or wholly before
+    // the frame's first block, the lane's chunk of that block)
+    auto lpos = [&](int rel, int lo) -> int { return kAl ? (rel >= lo ? rel : lo + 4 * (int)gl) : load_pos(rel, lo); };
 
     LaneKeys keys;
     {
@@ -1134,7 +1199,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     FS_RTSTAMP(5);
     FS_STAMP(0);
     TileA T;
-    u32x4 pf[kPrefetchA];
+    u32x4 pf[kPfA];
     const bool first = __builtin_amdgcn_readfirstlane(tile) < ntiles;
     {
         uint64_t S;
@@ -1148,7 +1213,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         FS_STAMP(8);
         T.P = 0;
         if (first) {
-            tile_geometry_a(T, tile, grp, gl, n, S, len, frames, fpt);
+            tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
             if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
         }
     }
@@ -1157,13 +1222,13 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     if (first) x4 = header_dma<true>(T, frames, lds, hw, gl, lane);
     if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-        for (int i = 0; i < kPrefetchA; ++i) {
+        for (int i = 0; i < kPfA; ++i) {
             const int rel = T.rel0 + kRowDwords * i;
-            pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
+            pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
         }
     }
     FS_STAMP(9);
-    tables_landed<kPrefetchA>(first, T.P > 0, x4);
+    tables_landed<kPfA>(first, T.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -1183,10 +1248,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
 
         // ---- header parse: after the first block of rows, while the ring's loads are in flight.
-        // The header DMA was issued before the tile's rows; vmcnt(kPrefetchA) retires it once the
+        // The header DMA was issued before the tile's rows; vmcnt(kPfA) retires it once the
         // first block's refills are the only younger loads.
         auto parse = [&](bool refilled) {
-            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPrefetchA);
+            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
             else __builtin_amdgcn_s_waitcnt(0x0070);
             parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
                        parser, hw);
@@ -1208,16 +1273,19 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             constexpr bool kRefill = decltype(refill_tag)::value;
             prio(r0);
 #pragma unroll
-            for (int i = 0; i < kPrefetchA; ++i) {
+            for (int i = 0; i < kPfA; ++i) {
                 const int r = r0 + i;
                 const int rel = T.rel0 + kRowDwords * r;
                 // consume the ring slot, then refill the SAME registers: no copy of an
-                // in-flight load, so the compiler keeps kPrefetchA-1 loads outstanding
-                if (r < T.H) masked_row(lds, keys, pf[i], rel, load_pos(rel, T.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
+                // in-flight load, so the compiler keeps kPfA-1 loads outstanding
+                const bool masked = r < T.H;
+                if (kAl && masked) masked_row_al(lds, keys, pf[i], rel, T.nd(), T.sa(), T.tail_mask(), A, cs);
+                else if (masked) masked_row(lds, keys, pf[i], rel, load_pos(rel, T.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
+                else if (kAl && !kRefill && i == kPfA - 1) tail_row_al(lds, keys, pf[i], rel, T.nd(), T.tail_mask(), A, cs);
                 else lean_row(lds, keys, pf[i], A, cs);
                 if (kRefill) {
-                    const int rn = rel + kRowDwords * kPrefetchA;
-                    pf[i] = load_row(T.gfb, r + kPrefetchA < T.H ? load_pos(rn, T.lo) : rn);
+                    const int rn = rel + kRowDwords * kPfA;
+                    pf[i] = load_row(T.gfb, r + kPfA < T.H ? lpos(rn, T.lo) : rn);
                 }
             }
         };
@@ -1226,10 +1294,12 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         auto lean_block = [&](int r0, auto refill_tag) {
             constexpr bool kRefill = decltype(refill_tag)::value;
             prio(r0);
-            const uint32_t* pb = T.gfb + (T.rel0 + kRowDwords * (r0 + kPrefetchA));
+            const uint32_t* pb = T.gfb + (T.rel0 + kRowDwords * (r0 + kPfA));
 #pragma unroll
-            for (int i = 0; i < kPrefetchA; ++i) {
-                lean_row(lds, keys, pf[i], A, cs);
+            for (int i = 0; i < kPfA; ++i) {
+                if (kAl && !kRefill && i == kPfA - 1)
+                    tail_row_al(lds, keys, pf[i], T.rel0 + kRowDwords * (r0 + i), T.nd(), T.tail_mask(), A, cs);
+                else lean_row(lds, keys, pf[i], A, cs);
                 if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
                 // keep consume/refill interleaved per row: unfenced, the scheduler sinks all
                 // refills to the block end behind a vmcnt(0), draining the ring every block
@@ -1238,16 +1308,16 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         };
         using Yes = std::true_type;
         using No = std::false_type;
-        const int Rc = T.P - kPrefetchA;  // first row of the last block
+        const int Rc = T.P - kPfA;  // first row of the last block
         if (T.P > 0) {
             // [first block] parse [head blocks: general] [body: lean] [last block: no refill]
             if (Rc > 0) {
                 if (T.H > 0) block(0, Yes());
                 else lean_block(0, Yes());
                 parse(true);
-                int r0 = kPrefetchA;
-                for (; r0 < Rc && r0 < T.H; r0 += kPrefetchA) block(r0, Yes());
-                for (; r0 < Rc; r0 += kPrefetchA) lean_block(r0, Yes());
+                int r0 = kPfA;
+                for (; r0 < Rc && r0 < T.H; r0 += kPfA) block(r0, Yes());
+                for (; r0 < Rc; r0 += kPfA) lean_block(r0, Yes());
                 if (Rc < T.H) block(Rc, No());
                 else lean_block(Rc, No());
             } else {
@@ -1268,14 +1338,33 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         // sad16 of it: remove both.
         // the parked parse, read by every lane now: its LDS round trip overlaps the combine's
         const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
-        uint32_t junk = 0u;
-        if (T.P > 0 && T.H < T.P && gl == 3u && T.nd() > 0) junk = pf[kPrefetchA - 1].w & ~T.tail_mask();
-        const uint32_t U =
-            zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3] ^ junk;
-        cs -= sad16(junk, 0u);
-        const uint32_t ybase = (gl == 0u) ? kLdsZ48 : (gl == 1u) ? kLdsZ32 : kLdsZ16;
-        uint32_t Y = zplain(lds, U, ybase);
-        if (gl == 3u) Y = U;
+        uint32_t Y;
+        if (kAl) {
+            // block-aligned rows: stream j of lane gl (row position 4 gl + j) is shifted by its
+            // distance in dwords to the frame's last dword, at position q = 15 - ealign() of the
+            // last row: (q - 4 gl - j) mod 16 (the streams past q skipped the last row), as
+            // Z_(16 a) Z_(4 c) with s = 4 a + c
+            const uint32_t kq = (uint32_t)(15 - T.ealign() - 4 * (int)gl);
+            Y = 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t sh = (kq - j) & 15u, c = sh & 3u, a4 = sh >> 2;
+                uint32_t v = A[j];
+                const uint32_t v1 = zplain(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
+                v = c ? v1 : v;
+                const uint32_t v2 = zplain(lds, v, a4 == 1u ? kLdsZ16 : a4 == 2u ? kLdsZ32 : kLdsZ48);
+                Y ^= a4 ? v2 : v;
+            }
+        } else {
+            uint32_t junk = 0u;
+            if (T.P > 0 && T.H < T.P && gl == 3u && T.nd() > 0) junk = pf[kPfA - 1].w & ~T.tail_mask();
+            const uint32_t U =
+                zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3] ^ junk;
+            cs -= sad16(junk, 0u);
+            const uint32_t ybase = (gl == 0u) ? kLdsZ48 : (gl == 1u) ? kLdsZ32 : kLdsZ16;
+            Y = zplain(lds, U, ybase);
+            if (gl == 3u) Y = U;
+        }
         Y ^= dpp_quad<kQuadXor1>(Y);
         Y ^= dpp_quad<kQuadXor2>(Y);
         // checksum over the 4 lanes of the group, each lane first folded mod 65535 (the finish
@@ -1296,14 +1385,14 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             uint32_t len;
             tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
             descriptors_ready<kOps>(S, len);
-            tile_geometry_a(T, tile, grp, gl, n, S, len, frames, fpt);
+            tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
             if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             header_dma<true>(T, frames, lds, hw, gl, lane);
             if (T.P > 0) {
 #pragma unroll
-                for (int i = 0; i < kPrefetchA; ++i) {
+                for (int i = 0; i < kPfA; ++i) {
                     const int rel = T.rel0 + kRowDwords * i;
-                    pf[i] = load_row(T.gfb, i < T.H ? load_pos(rel, T.lo) : rel);
+                    pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
                 }
             }
         }
@@ -2112,21 +2201,25 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #undef FS_LAUNCH_W
         return hipGetLastError();
     }
-#define FS_LAUNCH(K, OPS)                                                                                   \
-    hipLaunchKernelGGL((K<OPS>), dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
+#define FS_LAUNCH(K)                                                                                        \
+    hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
+    const bool al = force == 0 || force == 4;  // the one-pass choice: block-aligned rows (force 1: end-anchored)
     switch (op) {
     case FsOp::kDigest:
-        if (mixed) FS_LAUNCH(digest_kernel_ab, kOpsDigest);
-        else FS_LAUNCH(digest_kernel_a, kOpsDigest);
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
+        else if (al) FS_LAUNCH((digest_kernel_a<kOpsDigest, true>));
+        else FS_LAUNCH((digest_kernel_a<kOpsDigest, false>));
         break;
     case FsOp::kFill:
-        if (mixed) FS_LAUNCH(digest_kernel_ab, kOpsTx);
-        else FS_LAUNCH(digest_kernel_a, kOpsTx);
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
+        else if (al) FS_LAUNCH((digest_kernel_a<kOpsTx, true>));
+        else FS_LAUNCH((digest_kernel_a<kOpsTx, false>));
         break;
     case FsOp::kFcs:
-        if (mixed) FS_LAUNCH(digest_kernel_ab, kOpsFcs);
-        else FS_LAUNCH(digest_kernel_a, kOpsFcs);
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
+        else if (al) FS_LAUNCH((digest_kernel_a<kOpsFcs, true>));
+        else FS_LAUNCH((digest_kernel_a<kOpsFcs, false>));
         break;
     }
 #undef FS_LAUNCH

@@ -194,7 +194,7 @@ class Engine:
             raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
 
     # kernel variants (fs_ctx_set_kernel): results are identical, only the speed differs
-    KERNEL_AUTO, KERNEL_ONE_PASS, KERNEL_MIXED, KERNEL_WIDE = 0, 1, 2, 3
+    KERNEL_AUTO, KERNEL_ONE_PASS, KERNEL_MIXED, KERNEL_WIDE, KERNEL_ALIGNED = 0, 1, 2, 3, 4
 
     def set_kernel(self, variant: int) -> None:
         """0: automatic (default: the 16-lane kernel); 1: the 4-lane one-pass kernel; 2: the

@@ -262,3 +262,57 @@ def crc32_model_w1(buf: bytes, S: int, length: int) -> int:
         Y ^= W if quad_level[q] is None else apply(quad_level[q], W)
     t = (4 - (E & 3)) & 3
     return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
+
+
+def crc32_model_al(buf: bytes, S: int, length: int, base_phase: int = 0) -> int:
+    """digest_kernel_a<kOps, true>: BLOCK-ALIGNED 64-byte rows (the last row ends on the 64-B
+    block after the frame end; base_phase = absolute dword phase of buf[0] within a block),
+    the stream dwords past the frame end leave their stream untouched, and the combine shifts
+    stream (lane, j) by 4 * ((q - 4 lane - j) mod 16) bytes, q = the frame's last dword's
+    position in the last row."""
+    E = S + length
+    if length < 4:
+        return crc32_model(buf, S, length)
+    sdw = S >> 2
+    nd = ((E + 3) >> 2) - sdw
+    sa = S & 3
+    te = (E & 3) or 4
+    head_mask = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
+    tail_mask = 0xFFFFFFFF if te == 4 else (1 << (8 * te)) - 1
+    padded = b"\0" * 64 + bytes(buf) + b"\0" * 72
+    ph = (base_phase + sdw) & 15
+    e = (16 - ((ph + nd) & 15)) & 15
+    ndb = nd + e
+    R = (ph + ndb) // 16
+
+    def dword(rel):
+        return struct.unpack_from("<I", padded, 64 + 4 * (sdw + rel))[0]
+
+    A = [[0] * 4 for _ in range(4)]
+    for r in range(R):
+        for lane in range(4):
+            rel = ndb - 16 * R + 16 * r + 4 * lane
+            for j in range(4):
+                x = rel + j
+                d = dword(x) if x >= 0 else 0
+                c = 0
+                if x == 0:
+                    d &= head_mask
+                    c = head_mask
+                if x == 1:
+                    c = ~head_mask & 0xFFFFFFFF
+                if x == nd - 1:
+                    d &= tail_mask
+                if x < nd:
+                    A[lane][j] = apply(Z64, A[lane][j]) ^ d ^ c
+    q = 15 - e
+    Y = 0
+    for lane in range(4):
+        for j in range(4):
+            s = (q - 4 * lane - j) & 15
+            v = A[lane][j]
+            if s:
+                v = apply(op_table(4 * s), v)
+            Y ^= v
+    t = (4 - (E & 3)) & 3
+    return apply(ZFIN[t], Y) ^ 0xFFFFFFFF

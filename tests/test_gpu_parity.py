@@ -21,11 +21,11 @@ from seqs_amd import Engine, pack_frames, split_digests, synth  # noqa: E402
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_WIDE,
+@pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_WIDE, Engine.KERNEL_ALIGNED,
                                         Engine.KERNEL_AUTO],
-                ids=["one_pass", "mixed", "wide", "auto"])
+                ids=["one_pass", "mixed", "wide", "aligned", "auto"])
 def engine(request):
-    # every case through both kernel variants (and the automatic choice between them)
+    # every case through every kernel variant (and the automatic choice)
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     e = Engine(0)

@@ -74,3 +74,24 @@ def test_l4_native_split_matches_reference():
         assert km.fold_native_to_be(total, parity) == got
         checked += 1
     assert checked > 100
+
+
+def test_block_aligned_rows_vs_zlib():
+    # digest_kernel_a<kOps, true>: rows on 64-B blocks, skipped updates past the frame end and
+    # the rotated combine reproduce zlib at every block phase, length and start alignment
+    rnd = random.Random(12)
+    for _ in range(300):
+        L = rnd.choice([4, 5, 7, 8, 15, 16, 17, 63, 64, 65, 127, 128, 129, 255, 256, 257, rnd.randrange(4, 1600)])
+        pre = rnd.randrange(0, 70)
+        buf = rnd.randbytes(pre + L + 8)
+        assert km.crc32_model_al(buf, pre, L, rnd.randrange(16)) == zlib.crc32(buf[pre : pre + L])
+
+
+def test_16_lane_models_vs_zlib():
+    rnd = random.Random(13)
+    for _ in range(150):
+        L = rnd.choice([4, 5, 255, 256, 257, 1500, rnd.randrange(4, 3000)])
+        pre = rnd.randrange(0, 13)
+        buf = rnd.randbytes(pre + L + 8)
+        assert km.crc32_model_w(buf, pre, L) == zlib.crc32(buf[pre : pre + L])
+        assert km.crc32_model_w1(buf, pre, L) == zlib.crc32(buf[pre : pre + L])
