@@ -99,7 +99,8 @@ def main():
                                      "gfx950 correction for wide coalesced reads; separate --pmc passes")
         cal = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "fetch_size_calibration.json")
         if "hbm_bytes_per_launch" in out and os.path.exists(cal):
-            f = json.load(open(cal))["pattern_factor"]
+            c = json.load(open(cal))
+            f = c["pattern_factor"][c["config_pattern"][cfg]]
             out["hbm_bytes_per_launch_calibrated"] = int(round(out["hbm_bytes_per_launch"] / f))
             out["calibration_note"] = (f"divided by {f}: the doubled FETCH_SIZE of this access pattern without "
                                        "compute over its true bytes (profiles/fetch_size_calibration.json)")

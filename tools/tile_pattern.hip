@@ -3,9 +3,11 @@
 // to back, as the C2/C4 batches), G lanes per frame, rows of 16*G bytes, a ring of PF row
 // loads per wave that runs on across tiles (no drain at tile ends). Rows either aligned to
 // their size in memory (AL = 1: full 128-B lines for G >= 8; the partial head and tail rows'
-// lanes outside the frame issue no load) or anchored at the frame end (AL = 0, the current
-// kernel's rows for G = 4). Compared with a plain grid-stride stream, on a 98.3 MB C2 batch
-// (one launch) and a 1.57 GB C4 batch (steady state), on 1 and 4 streams.
+// lanes outside the frame issue no load; AL = 2: whole blocks, every lane loads -- the one-pass
+// kernel's block-aligned rows for G = 4) or anchored at the frame end (AL = 0, the end-anchored
+// rows). Compared with a plain grid-stride stream, on a 98.3 MB C2 batch (one launch) and a
+// 1.57 GB C4 batch (steady state), on 1 and 4 streams. `tile_pattern calib`: the FETCH_SIZE
+// calibration set (run under rocprofv3 --pmc FETCH_SIZE).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -26,7 +28,7 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
         }                                                                                 \
     } while (0)
 
-template <int G, int PF, bool AL, int WPB>
+template <int G, int PF, int AL, int WPB>
 __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
                                                     uint32_t* out) {
     constexpr int FPT = 64 / G;
@@ -49,7 +51,7 @@ __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ 
             const uint64_t b0 = S / RB, b1 = (E - 1) / RB;
             if (b0 + (uint64_t)r > b1) return false;
             a = (b0 + r) * RB + 16u * gl;
-            if (a + 16 <= S || a >= E) return false;
+            if (AL == 1 && (a + 16 <= S || a >= E)) return false;  // AL 2: whole blocks, as the kernel loads
         } else {
             const uint64_t E4 = (E + 3) & ~uint64_t(3);
             const int64_t s = (int64_t)E4 - (int64_t)RB * (Rmax - r) + 16 * (int64_t)gl;
@@ -102,6 +104,7 @@ int main(int argc, char** argv) {
     const bool big = argc > 1 && std::string(argv[1]) == "c4";
     const uint32_t nf = big ? (1u << 20) : 65536u;
     const size_t nbytes = (size_t)nf * flen;
+    const bool calib = argc > 1 && std::string(argv[1]) == "calib";
     const int NB = big ? 2 : 6;
     std::vector<uint8_t*> bufs(NB);
     for (auto& b : bufs) {
@@ -116,7 +119,7 @@ int main(int argc, char** argv) {
     hipStream_t st[4];
     for (auto& x : st) CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     printf("batch %u x %u B = %zu bytes, %d rotated, %d CUs\n", nf, flen, nbytes, NB, cus);
-    const int reps = big ? 40 : 400;
+    const int reps = big ? 40 : calib ? 20 : 400;
     auto run = [&](auto launch, const char* name) {
         double res[2];
         int k = 0;
@@ -133,33 +136,34 @@ int main(int argc, char** argv) {
         printf("%-44s 1 stream %9.2f us %7.0f GB/s | 4 streams %9.2f us %7.0f GB/s\n", name, res[0],
                nbytes / (res[0] * 1e-6) / 1e9, res[1], nbytes / (res[1] * 1e-6) / 1e9);
     };
-#define TILES(G, PF, AL, WPB)                                                                              \
+#define TILES(G, PF, AL, WPB) TILESX(G, PF, AL, WPB, 1)
+#define TILESX(G, PF, AL, WPB, GM)                                                                        \
     run([&](int i, hipStream_t s) {                                                                       \
-        hipLaunchKernelGGL((k_tiles<G, PF, AL, WPB>), dim3(cus), dim3(64 * WPB), 0, s, bufs[i % NB], nf, flen, out); \
-    }, "tiles G=" #G " PF=" #PF " AL=" #AL " waves/CU=" #WPB)
+        hipLaunchKernelGGL((k_tiles<G, PF, AL, WPB>), dim3(cus * GM), dim3(64 * WPB), 0, s, bufs[i % NB], nf, flen, out); \
+    }, "tiles G=" #G " PF=" #PF " AL=" #AL " waves/WG=" #WPB " WG/CU=" #GM)
 #define STREAM(PF, WPB, GRIDMUL)                                                                          \
     run([&](int i, hipStream_t s) {                                                                       \
         hipLaunchKernelGGL((k_stream<PF, WPB>), dim3(cus * GRIDMUL), dim3(64 * WPB), 0, s,                \
                            (const u32x4*)bufs[i % NB], nbytes / 16, out);                                 \
     }, "stream PF=" #PF " waves/WG=" #WPB " WG/CU=" #GRIDMUL)
+    if (calib) {  // FETCH_SIZE calibration under rocprofv3 (98,304,000 B per launch)
+        STREAM(4, 16, 1);
+        TILES(4, 5, 2, 16);
+        TILES(4, 6, 0, 16);
+        return 0;
+    }
     STREAM(4, 4, 2);
-    STREAM(6, 16, 1);
     STREAM(4, 16, 1);
+    TILES(4, 5, 2, 16);
     TILES(4, 6, false, 16);
-    TILES(4, 6, true, 16);
-    TILES(8, 6, true, 16);
-    TILES(8, 4, true, 16);
-    TILES(8, 8, true, 16);
-    TILES(16, 4, true, 16);
-    TILES(16, 6, true, 16);
+    TILES(4, 5, true, 16);
+    TILESX(4, 5, true, 16, 2);
+    TILESX(4, 5, true, 8, 2);
+    TILESX(4, 5, true, 8, 4);
+    TILES(4, 10, true, 16);
+    TILESX(4, 10, true, 8, 2);
+    TILESX(4, 5, false, 16, 2);
     TILES(16, 6, false, 16);
-    TILES(32, 4, true, 16);
-    TILES(64, 4, true, 16);
-    TILES(64, 6, true, 16);
-    TILES(64, 4, false, 16);
-    TILES(8, 6, true, 8);
-    TILES(16, 8, true, 8);
-    TILES(4, 6, false, 16);
-    STREAM(4, 4, 2);
+    TILESX(16, 4, false, 16, 2);
     return 0;
 }
