@@ -75,6 +75,12 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_EARLY_TABLES
 #define FS_EARLY_TABLES 1  // the plain-table DMA right behind the descriptor loads (0: after the geometry)
 #endif
+#ifndef FS_ROWS_FIRST
+#define FS_ROWS_FIRST 0  // one-pass kernel: the first tile's rows before its header DMA (measured: within noise)
+#endif
+#ifndef FS_LATE_REPORT
+#define FS_LATE_REPORT 0  // one-pass kernel: the mixed-length report after the parse (measured slower)
+#endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio per block of rows
 #endif
@@ -1214,19 +1220,28 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         T.P = 0;
         if (first) {
             tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
-            if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+            FS_STAMP(11);
+            if (!FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+            FS_STAMP(12);
         }
     }
     if (!FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);
     bool x4 = false;
-    if (first) x4 = header_dma<true>(T, frames, lds, hw, gl, lane);
-    if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
+    auto first_rows = [&]() {
+        if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-        for (int i = 0; i < kPfA; ++i) {
-            const int rel = T.rel0 + kRowDwords * i;
-            pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
+            for (int i = 0; i < kPfA; ++i) {
+                const int rel = T.rel0 + kRowDwords * i;
+                pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
+            }
         }
-    }
+    };
+    // (FS_ROWS_FIRST: the first rows before the header DMA -- still older than the first
+    // block's refills, which is all the parse's vmcnt(kPfA) needs; measured within noise)
+    if (FS_ROWS_FIRST) first_rows();
+    if (first) x4 = header_dma<true>(T, frames, lds, hw, gl, lane);
+    FS_STAMP(13);
+    if (!FS_ROWS_FIRST) first_rows();
     FS_STAMP(9);
     tables_landed<kPfA>(first, T.P > 0, x4);
     FS_STAMP(10);
@@ -1255,6 +1270,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             else __builtin_amdgcn_s_waitcnt(0x0070);
             parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
                        parser, hw);
+            if (FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
         };
         auto prio = [&](int r0) {
             // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
@@ -1386,7 +1402,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
             descriptors_ready<kOps>(S, len);
             tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
-            if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+            if (!FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             header_dma<true>(T, frames, lds, hw, gl, lane);
             if (T.P > 0) {
 #pragma unroll

@@ -58,7 +58,9 @@ print(f"  realtime: span {us(re_.max() - t0):.2f} us; wave start offset p50/p90/
 print(f"  memtime ticks per us (median over waves): {np.median((s[:, 4] - s[:, 0]) / np.maximum(1, us(re_ - rs))):.0f}")
 if s[:, 9].any():
     for nm, a_, b_ in (("start->regionA", 0, 7), ("regionA->desc", 7, 8), ("start->desc (fine)", 0, 8), ("desc->geom+issue", 8, 9), ("start->geom+issue", 0, 9),
-                       ("issue->waitcnt", 9, 10), ("waitcnt->barrier", 10, 1)):
+                       ("issue->waitcnt", 9, 10), ("waitcnt->barrier", 10, 1),
+                       ("desc->geometry", 8, 11), ("geometry->report", 11, 12), ("report->header", 12, 13),
+                       ("header->rows issued", 13, 9)):
         if s[:, b_].any() and s[:, a_].any():
             d = s[:, b_] - s[:, a_]
             print(f"  {nm:18s} median {int(np.median(d)):8d}  p10 {int(np.percentile(d, 10)):8d}  p90 {int(np.percentile(d, 90)):8d}")
