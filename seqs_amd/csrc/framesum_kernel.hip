@@ -896,7 +896,11 @@ __device__ __forceinline__ void full_piece_unit(Unit& U, const char* lds, const 
 // kernel's report)
 __device__ __forceinline__ bool mode_b_worthy(int nd) {
     const int rows = (nd + kRowDwords - 1) / kRowDwords;
-    const int RA = (group_max(rows) + kPrefetch - 1) / kPrefetch * kPrefetch;
+    const int rmax = group_max(rows);
+    // a tile whose frames differ by under 4 rows (256 B) has nothing for pieces to fill: the
+    // common case of uniform batches skips the piece arithmetic (it only steers the choice)
+    if (rmax + group_max(-rows) < 4) return false;
+    const int RA = (rmax + kPrefetch - 1) / kPrefetch * kPrefetch;
     const int npc = nd > 0 ? pieces_of(nd) : 1;
     const int nd0 = nd - kPieceDwords * (npc - 1);
     const int P0B = (group_max((nd0 + kRowDwords - 1) / kRowDwords) + kPrefetch - 1) / kPrefetch * kPrefetch;
