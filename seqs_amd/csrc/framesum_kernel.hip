@@ -81,6 +81,10 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_LATE_REPORT
 #define FS_LATE_REPORT 0  // one-pass kernel: the mixed-length report after the parse (measured slower)
 #endif
+#ifndef FS_CHAIN
+#define FS_CHAIN 0  // block-aligned one-pass kernel: chained tiles (the ring runs on across a wave's
+                    // tiles); parity-green, C4 within noise of the unchained kernel
+#endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio per block of rows
 #endif
@@ -135,6 +139,7 @@ constexpr uint32_t kWaveScratchBytes = 16u * kFramesPerTile + 8u * kFramesPerTil
                                        8u * (kFramesPerTile + kFramesPerTile * kMaxFullPasses);
 constexpr uint32_t kLdsWave = kLdsHdr + kWavesPerBlock * kHdrWaveBytes;
 constexpr uint32_t kLdsBytes = kLdsWave + kWavesPerBlock * kWaveScratchBytes;
+static_assert(kWaveScratchBytes >= 3u * 256u, "a parked parse (12 dwords x 16 frames, header-slot layout) fits the wave scratch");
 static_assert(kPieceRows % kPrefetch == 0, "a piece is whole blocks of rows");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kTablesLdsBytes == kLdsTables, "FsTables is the LDS image of the tables");
@@ -1184,6 +1189,11 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     fpt = __builtin_amdgcn_readfirstlane(fpt);
     const uint32_t ntiles = (n + fpt - 1) / fpt;
     const uint32_t hw = kLdsHdr + wave * kHdrWaveBytes;  // this wave's header slots
+    // where the parse is parked until the finish: the header slot itself, or with chained tiles
+    // (the next tile's header DMA lands before this tile's finish) the wave's scratch area,
+    // which the one-pass kernel does not otherwise use
+    constexpr bool kChain = kAl && FS_CHAIN;
+    const uint32_t pk = kChain ? kLdsWave + wave * kWaveScratchBytes : hw;
     // where a masked row's chunk is loaded (block-aligned rows: where it lies, or wholly before
     // the frame's first block, the lane's chunk of that block)
     auto lpos = [&](int rel, int lo) -> int { return kAl ? (rel >= lo ? rel : lo + 4 * (int)gl) : load_pos(rel, lo); };
@@ -1265,6 +1275,18 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         uint32_t cs = 0u;
         const bool fvalid = grp < fpt && tile * fpt + grp < n;
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
+        const int Rc = T.P - kPfA;  // first row of the last block
+        // Chained tiles (block-aligned kernel): the next tile's descriptors are loaded right after
+        // this tile's parse, its geometry is set up before the last block, and the last block
+        // refills the ring with the next tile's first rows, so the ring never drains between a
+        // wave's tiles. It needs a block of refills between the parse and the last block (the
+        // descriptors must be older than the ring's loads there): tiles of 3+ blocks.
+        const uint32_t tnext = tile + nwaves;
+        const bool chain = kChain && tnext < ntiles && Rc >= 2 * kPfA;
+        uint64_t Sn = 0;
+        uint32_t lenn = 0;
+        TileA Tn;
+        Tn.P = 0;
 
         // ---- header parse: after the first block of rows, while the ring's loads are in flight.
         // The header DMA was issued before the tile's rows; vmcnt(kPfA) retires it once the
@@ -1273,8 +1295,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
             else __builtin_amdgcn_s_waitcnt(0x0070);
             parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
-                       parser, hw);
+                       parser, pk);
             if (FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+            if (chain) tile_descriptors(tnext, grp, n, offsets, lengths, Sn, lenn, fpt);
         };
         auto prio = [&](int r0) {
             // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
@@ -1288,9 +1311,11 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             }
         };
         // general block: rows below H take the masked path (scalar branch per row); refills
-        // of rows below H are clamped
+        // of rows below H are clamped. Refill kind: 0 none (the tile's last block), 1 this
+        // tile's rows kPfA ahead, 2 the next tile's first rows (the last block, chained).
         auto block = [&](int r0, auto refill_tag) {
-            constexpr bool kRefill = decltype(refill_tag)::value;
+            constexpr int kKind = decltype(refill_tag)::value;
+            constexpr bool kRefill = kKind == 1;
             prio(r0);
 #pragma unroll
             for (int i = 0; i < kPfA; ++i) {
@@ -1306,13 +1331,17 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 if (kRefill) {
                     const int rn = rel + kRowDwords * kPfA;
                     pf[i] = load_row(T.gfb, r + kPfA < T.H ? lpos(rn, T.lo) : rn);
+                } else if (kKind == 2) {
+                    const int rn = Tn.rel0 + kRowDwords * i;
+                    pf[i] = load_row(Tn.gfb, i < Tn.H ? lpos(rn, Tn.lo) : rn);
                 }
             }
         };
         // lean block: every row lean for every lane; the refills lie inside the frame, so they
         // need no clamp: one pointer per block, immediate row offsets
         auto lean_block = [&](int r0, auto refill_tag) {
-            constexpr bool kRefill = decltype(refill_tag)::value;
+            constexpr int kKind = decltype(refill_tag)::value;
+            constexpr bool kRefill = kKind == 1;
             prio(r0);
             const uint32_t* pb = T.gfb + (T.rel0 + kRowDwords * (r0 + kPfA));
 #pragma unroll
@@ -1320,15 +1349,20 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 if (kAl && !kRefill && i == kPfA - 1)
                     tail_row_al(lds, keys, pf[i], T.rel0 + kRowDwords * (r0 + i), T.nd(), T.tail_mask(), A, cs);
                 else lean_row(lds, keys, pf[i], A, cs);
-                if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
+                if (kRefill) {
+                    pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
+                } else if (kKind == 2) {
+                    const int rn = Tn.rel0 + kRowDwords * i;
+                    pf[i] = load_row(Tn.gfb, i < Tn.H ? lpos(rn, Tn.lo) : rn);
+                }
                 // keep consume/refill interleaved per row: unfenced, the scheduler sinks all
                 // refills to the block end behind a vmcnt(0), draining the ring every block
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
-        using Yes = std::true_type;
-        using No = std::false_type;
-        const int Rc = T.P - kPfA;  // first row of the last block
+        using Yes = std::integral_constant<int, 1>;
+        using No = std::integral_constant<int, 0>;
+        using Next = std::integral_constant<int, 2>;
         if (T.P > 0) {
             // [first block] parse [head blocks: general] [body: lean] [last block: no refill]
             if (Rc > 0) {
@@ -1338,8 +1372,21 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 int r0 = kPfA;
                 for (; r0 < Rc && r0 < T.H; r0 += kPfA) block(r0, Yes());
                 for (; r0 < Rc; r0 += kPfA) lean_block(r0, Yes());
-                if (Rc < T.H) block(Rc, No());
-                else lean_block(Rc, No());
+                if (chain) {
+                    // the next tile's descriptors are older than the ring's kPfA loads
+                    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(Sn), "+v"(lenn) : "n"(kPfA));
+                    if (kOps == kOpsFcs) lenn = lenn >= 4u ? lenn - 4u : 0u;
+                    tile_geometry_a<kAl>(Tn, tnext, grp, gl, n, Sn, lenn, frames, fpt);
+                    if (report && mode_b_worthy(Tn.nd()) && lane == 0u) post_report(report);
+                    if (Rc < T.H) block(Rc, Next());
+                    else lean_block(Rc, Next());
+                    // this tile's header slot is free (its parse is parked in the wave scratch)
+                    header_dma<true>(Tn, frames, lds, hw, gl, lane);
+                } else if (Rc < T.H) {
+                    block(Rc, No());
+                } else {
+                    lean_block(Rc, No());
+                }
             } else {
                 if (T.H > 0) block(0, No());
                 else lean_block(0, No());
@@ -1357,7 +1404,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         // that junk itself (the last dword enters the combine unshifted) and their sum is
         // sad16 of it: remove both.
         // the parked parse, read by every lane now: its LDS round trip overlaps the combine's
-        const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
+        const Parsed P = unpark_parsed<kOps>(lds, pk, grp);
         uint32_t Y;
         if (kAl) {
             // block-aligned rows: stream j of lane gl (row position 4 gl + j) is shifted by its
@@ -1399,8 +1446,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                                tile * fpt + grp, out, status, tx);
         FS_STAMP(4);
         FS_RTSTAMP(6);
-        tile += nwaves;
-        if (tile < ntiles) {  // next tile: descriptors, geometry, header DMA, row prefetch
+        tile = tnext;
+        if (chain) {
+            T = Tn;  // its first rows are in the ring, its header DMA issued
+        } else if (tile < ntiles) {  // next tile: descriptors, geometry, header DMA, row prefetch
             uint64_t S;
             uint32_t len;
             tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
