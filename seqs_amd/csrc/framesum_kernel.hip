@@ -81,6 +81,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_LATE_REPORT
 #define FS_LATE_REPORT 0  // one-pass kernel: the mixed-length report after the parse (measured slower)
 #endif
+#ifndef FS_HDR_AL
+#define FS_HDR_AL 32  // block-aligned one-pass kernel: header slot dwords (16 or 32; 16 measured within noise)
+#endif
 #ifndef FS_CHAIN
 #define FS_CHAIN 0  // block-aligned one-pass kernel: chained tiles (the ring runs on across a wave's
                     // tiles); parity-green, C4 within noise of the unchained kernel
@@ -113,7 +116,6 @@ constexpr int kRingA = kAl ? kPrefetchAl : kPrefetchA;
 // so the DMA destination is lane-linear and both the parser lanes (one per group, same x)
 // and the group-vectorised sums (lane gl reads x = 4i + gl) read conflict-free.
 constexpr int kHdrDwords = 32;
-constexpr int kHdrDmas = kHdrDwords / 4;
 constexpr uint32_t kHdrWaveBytes = 4u * kHdrDwords * kFramesPerTile;  // 2 KB
 
 // LDS map (bytes). [0, 104 KB) holds the tables: the plain tables first (copied by LDS-DMA
@@ -1089,15 +1091,16 @@ __device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, con
 // Returns whether the dwordx4 form was used (wave-uniform: 2 instructions, else 8). kX4 = false
 // (the mixed-length kernel: its tiles hold short frames, and the permutes cost it registers)
 // always takes the dword form.
-template <bool kX4, class TileT>
+template <bool kX4, int kSlot = kHdrDwords, class TileT>
 __device__ __forceinline__ bool header_dma(const TileT& T, const uint8_t* __restrict__ frames, const char* lds,
                                            uint32_t hw, uint32_t gl, uint32_t lane) {
+    static_assert(kSlot == 16 || kSlot == 32, "header slot: 16 or 32 dwords");
     if (FS_DIAG & 1) return false;
     const uint32_t hdr0 = __builtin_amdgcn_readfirstlane(lds_base(lds) + hw);
     const int last = T.ndall() - 1;
     const bool own = T.len > 0u;
     const uint64_t fa = reinterpret_cast<uint64_t>(frames + (T.sdw() << 2));
-    if (kX4 && __ballot(own && last < kHdrDwords - 1) == 0) {
+    if (kX4 && __ballot(own && last < kSlot - 1) == 0) {
         const int src = (int)((lane & 15u) << 4);  // group (lane & 15)'s lane 0
         const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)fa);
         const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(fa >> 32));
@@ -1106,14 +1109,14 @@ __device__ __forceinline__ bool header_dma(const TileT& T, const uint8_t* __rest
         const uint32_t q = lane >> 4;
         if (lg > 0u) {
             dma_x4(fb + 4u * q, hdr0);
-            dma_x4(fb + 4u * (q + 4u), hdr0 + 1024u);
+            if (kSlot > 16) dma_x4(fb + 4u * (q + 4u), hdr0 + 1024u);
         }
         return true;
     }
     if (own) {  // exec-masked: a group with no frame bytes writes nothing (its slot is never used)
         const uint32_t* fbs = reinterpret_cast<const uint32_t*>(fa);
 #pragma unroll
-        for (int i = 0; i < kHdrDmas; ++i) dma_x1(fbs + min(4 * i + (int)gl, last), hdr0 + 256u * i);
+        for (int i = 0; i < kSlot / 4; ++i) dma_x1(fbs + min(4 * i + (int)gl, last), hdr0 + 256u * i);
     }
     return false;
 }
@@ -1121,12 +1124,13 @@ __device__ __forceinline__ bool header_dma(const TileT& T, const uint8_t* __rest
 // The preamble's wait: the table pieces (issued before the header DMA and the rows) have
 // landed -- vmcnt(rows + header DMAs) -- and lgkmcnt(0): this wave's region-A stores.
 // s_waitcnt field layout (gfx9): vmcnt[3:0] + vmcnt_hi[15:14], expcnt[6:4], lgkmcnt[11:8]
-template <int kPf>
+template <int kPf, int kSlot = kHdrDwords>
 __device__ __forceinline__ void tables_landed(bool first, bool rows, bool x4) {
-    if (first && rows && x4) __builtin_amdgcn_s_waitcnt(0x0070 | (kPf + 2));
-    else if (first && rows) __builtin_amdgcn_s_waitcnt(0x0070 | (kPf + kHdrDmas));
-    else if (first && x4) __builtin_amdgcn_s_waitcnt(0x0070 | 2);
-    else if (first) __builtin_amdgcn_s_waitcnt(0x0070 | kHdrDmas);
+    constexpr int kX4n = kSlot / 16, kX1n = kSlot / 4;  // header DMA instructions of either form
+    if (first && rows && x4) __builtin_amdgcn_s_waitcnt(0x0070 | (kPf + kX4n));
+    else if (first && rows) __builtin_amdgcn_s_waitcnt(0x0070 | (kPf + kX1n));
+    else if (first && x4) __builtin_amdgcn_s_waitcnt(0x0070 | kX4n);
+    else if (first) __builtin_amdgcn_s_waitcnt(0x0070 | kX1n);
     else __builtin_amdgcn_s_waitcnt(0x0070);
 }
 
@@ -1177,6 +1181,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx, uint32_t fpt) {
     char* lds = g_lds;
     constexpr int kPfA = kRingA<kAl>;
+    // header slot dwords (FS_HDR_AL = 16 with block-aligned rows: one dwordx4 DMA per wave, the
+    // parse reading the rare bytes past the slot from global memory; measured within noise of 32)
+    constexpr int kSlotA = kAl ? FS_HDR_AL : kHdrDwords;
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
@@ -1253,11 +1260,11 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     // (FS_ROWS_FIRST: the first rows before the header DMA -- still older than the first
     // block's refills, which is all the parse's vmcnt(kPfA) needs; measured within noise)
     if (FS_ROWS_FIRST) first_rows();
-    if (first) x4 = header_dma<true>(T, frames, lds, hw, gl, lane);
+    if (first) x4 = header_dma<true, kSlotA>(T, frames, lds, hw, gl, lane);
     FS_STAMP(13);
     if (!FS_ROWS_FIRST) first_rows();
     FS_STAMP(9);
-    tables_landed<kPfA>(first, T.P > 0, x4);
+    tables_landed<kPfA, kSlotA>(first, T.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -1294,7 +1301,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         auto parse = [&](bool refilled) {
             if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
             else __builtin_amdgcn_s_waitcnt(0x0070);
-            parse_tile<kOps>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
+            parse_tile<kOps, kSlotA>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
                        parser, pk);
             if (FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             if (chain) tile_descriptors(tnext, grp, n, offsets, lengths, Sn, lenn, fpt);
@@ -1381,7 +1388,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                     if (Rc < T.H) block(Rc, Next());
                     else lean_block(Rc, Next());
                     // this tile's header slot is free (its parse is parked in the wave scratch)
-                    header_dma<true>(Tn, frames, lds, hw, gl, lane);
+                    header_dma<true, kSlotA>(Tn, frames, lds, hw, gl, lane);
                 } else if (Rc < T.H) {
                     block(Rc, No());
                 } else {
@@ -1456,7 +1463,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             descriptors_ready<kOps>(S, len);
             tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
             if (!FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
-            header_dma<true>(T, frames, lds, hw, gl, lane);
+            header_dma<true, kSlotA>(T, frames, lds, hw, gl, lane);
             if (T.P > 0) {
 #pragma unroll
                 for (int i = 0; i < kPfA; ++i) {
