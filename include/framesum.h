@@ -118,7 +118,8 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
  *   FS_FILL_CSUM  writes the IPv4 header checksum (eth/headers.go:333-340) to frame[24:26]
  *                 and the TCP/UDP checksum RecvEth verifies (the same arithmetic, with the
  *                 frame's own TCP options; none when the data offset is 5, as :193 passes
- *                 nil) to the L4 checksum field, both big-endian, for every frame whose
+ *                 nil; frames with options are an extension of the reference's TX path,
+ *                 parity unpinned) to the L4 checksum field, both big-endian, for every frame whose
  *                 RecvEth evaluation reaches the checksum compare (verdict FS_OK or
  *                 FS_ERR_CHECKSUM before the fill); other frames are not written.
  *   FS_FCS_APPEND writes the IEEE CRC-32 of the frame (as filled) little-endian at
