@@ -218,7 +218,11 @@ def main():
     nb = len(batches)
     ns = max(1, args.streams)
     gather = dist.is_initialized() and not args.no_gather
-    main_stream = torch.cuda.current_stream(dev)
+    # every launch goes to created (non-blocking) streams, never the legacy default stream: a
+    # launch there costs about 5 us more, and a short timed region (the driver's 20 steps) pays
+    # it on every stream's first launch (tools/sync_overhead.py: 20.5-20.8 against 22.0-22.4 us
+    # per step at K = 20; no difference at K = 200)
+    main_stream = torch.cuda.Stream(dev)
     streams = [main_stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
     # Output slots (digest words, then verdicts, in one 256-B-aligned slab per slot). Without a
     # gather, step i writes slot i % nslot and slot k is only ever written by stream k (nslot ==
@@ -437,7 +441,7 @@ def main_c4(args, world, rank, local, dev):
         dist.all_reduce(t)
     bytes_global = int(t.item())
     gather = dist.is_initialized()
-    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]  # created streams (see main())
     # slot k: rank 0 gathers into recv[k] (world slabs back to back; its own slab is slab 0),
     # other ranks digest into send[k]
     recv = [torch.empty(world * sb, dtype=torch.uint8, device=dev) for _ in range(2)] if rank == 0 else None

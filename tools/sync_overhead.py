@@ -12,6 +12,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--spin", action="store_true")
 p.add_argument("--yield_", action="store_true")
 p.add_argument("--streams", type=int, default=4)
+p.add_argument("--pool", action="store_true", help="no launch on the default stream")
 a = p.parse_args()
 if a.spin or a.yield_:
     hip = ctypes.CDLL("libamdhip64.so")
@@ -28,7 +29,8 @@ for b in range(4):
     buf, off, ln = synth.uniform_batch(65536, 1500, seed=1 + b)
     bs.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)))
 e = Engine(0)
-streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(a.streams - 1)]
+streams = ([torch.cuda.Stream(dev) for _ in range(a.streams)] if a.pool else
+           [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(a.streams - 1)])
 outs = [torch.empty((65536, 2), dtype=torch.int32, device=dev) for _ in range(4)]
 sts = [torch.empty((65536,), dtype=torch.uint8, device=dev) for _ in range(4)]
 
@@ -40,7 +42,7 @@ def run(k):
 
 run(600)
 torch.cuda.synchronize()
-for k in (0, 1, 20, 20, 20, 200):
+for k in (0, 1, 2, 3, 4, 5, 6, 8, 12, 20, 20, 200):
     ts = []
     for rep in range(5):
         torch.cuda.synchronize()
