@@ -88,6 +88,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FS_CHAIN 0  // block-aligned one-pass kernel: chained tiles (the ring runs on across a wave's
                     // tiles); parity-green, C4 within noise of the unchained kernel
 #endif
+#ifndef FS_PRIO_MIN
+#define FS_PRIO_MIN 36  // ... for tiles of more rows than this
+#endif
 #ifndef FS_PRIO
 #define FS_PRIO 1  // progress-based s_setprio per block of rows
 #endif
@@ -1309,7 +1312,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         auto prio = [&](int r0) {
             // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
             // a wave with more rows left gets a higher priority.
-            if (FS_PRIO && T.P > 36) {  // long tiles only (C2-size tiles run faster without)
+            if (FS_PRIO && T.P > FS_PRIO_MIN) {  // long tiles only (C2-size tiles run faster without)
                 const int left4 = (4 * (T.P - r0)) / max(T.P, 1);  // 4 .. 1
                 if (left4 >= 4) __builtin_amdgcn_s_setprio(3);
                 else if (left4 == 3) __builtin_amdgcn_s_setprio(2);
