@@ -81,6 +81,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_LATE_REPORT
 #define FS_LATE_REPORT 0  // one-pass kernel: the mixed-length report after the parse (measured slower)
 #endif
+#ifndef FS_HDR_CAPTURE
+#define FS_HDR_CAPTURE 1  // block-aligned one-pass kernel: header slots captured from the first rows (no header DMA)
+#endif
 #ifndef FS_HDR_AL
 #define FS_HDR_AL 32  // block-aligned one-pass kernel: header slot dwords (16 or 32; 16 measured within noise)
 #endif
@@ -374,17 +377,20 @@ __device__ __forceinline__ uint32_t hdr_at(uint32_t hw, uint32_t g, uint32_t x) 
 __device__ __forceinline__ uint32_t hdr_dw(const char* lds, uint32_t hw, uint32_t g, uint32_t x) {
     return lds32(lds, hdr_at(hw, g, x));
 }
-// frame bytes [4j, 4j+4) as a little-endian dword (slot dwords are absolute, sa = S & 3)
-__device__ __forceinline__ uint32_t frame_dw(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t j) {
-    return __builtin_amdgcn_alignbyte(hdr_dw(lds, hw, g, j + 1), hdr_dw(lds, hw, g, j), sa);
+// frame bytes [4j, 4j+4) as a little-endian dword (slot dwords are absolute, sa = S & 3). `xo`:
+// the slot dword that holds frame dword 0 (0 for the DMA'd slot; the block phase for a slot
+// captured from block-aligned rows, which starts at the frame's first 64-B block)
+__device__ __forceinline__ uint32_t frame_dw(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t j,
+                                             uint32_t xo = 0u) {
+    return __builtin_amdgcn_alignbyte(hdr_dw(lds, hw, g, xo + j + 1), hdr_dw(lds, hw, g, xo + j), sa);
 }
 
 // frame_dw for a slot of kSlotDw dwords: dwords past the slot come from global memory,
 // clamped to the frame's last dword `last` as the DMA clamps them.
 template <int kSlotDw>
 __device__ __forceinline__ uint32_t frame_dw_t(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t j,
-                                               const uint32_t* fb, uint32_t last) {
-    if (kSlotDw >= 32 || j + 1 < (uint32_t)kSlotDw) return frame_dw(lds, hw, g, sa, j);
+                                               const uint32_t* fb, uint32_t last, uint32_t xo = 0u) {
+    if (kSlotDw >= 32 || j + 1 < (uint32_t)kSlotDw) return frame_dw(lds, hw, g, sa, j, xo);
     const uint32_t a = fb[min(j, last)], b = fb[min(j + 1u, last)];
     return __builtin_amdgcn_alignbyte(b, a, sa);
 }
@@ -393,12 +399,12 @@ __device__ __forceinline__ uint32_t frame_dw_t(const char* lds, uint32_t hw, uin
 // first 4*nx dwords, split over the group's 4 lanes (lane gl takes dwords 4i + gl) and
 // totalled over the group by DPP. Every lane of the group calls it with the same arguments.
 __device__ __forceinline__ uint32_t slot_sum(const char* lds, uint32_t hw, uint32_t g, uint32_t gl, uint32_t sa,
-                                             int p0, int p1, int nx) {
+                                             int p0, int p1, int nx, uint32_t xo = 0u) {
     const int a0 = (int)sa + p0, a1 = (int)sa + p1;
     uint32_t s = 0;
     for (int i = 0; i < nx; ++i) {
         const int x = 4 * i + (int)gl;
-        s = sad16(lds32(lds, hw + ((uint32_t)i << 8) + (g << 4) + (gl << 2)) & range_mask(x, a0, a1), s);
+        s = sad16(hdr_dw(lds, hw, g, xo + (uint32_t)x) & range_mask(x, a0, a1), s);
     }
     s += dpp_quad<kQuadXor1>(s);
     s += dpp_quad<kQuadXor2>(s);
@@ -434,13 +440,13 @@ struct Parsed {
 // (pad < 0: the padding lies past the slot, summed here from global memory).
 template <uint32_t kOps, int kSlotDw = kHdrDwords>
 __device__ __forceinline__ Parsed parse_frame(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t len, uint32_t mtu,
-                              uint32_t hsum, int64_t pad, const uint32_t* fb) {
+                              uint32_t hsum, int64_t pad, const uint32_t* fb, uint32_t xo = 0u) {
     Parsed r = {V_OK, 0u, 0u, 0, 0, 0u, 0u, 0, 0, 0u};
     if (len < 34u) { r.verdict = V_SMOL; return r; }                          // portstack.go:167-168
     if (mtu != 0 && len > mtu) { r.verdict = V_MTU; return r; }              // :169-172
     uint32_t bs[9];                                                           // bswap32(frame dword j), j = 3..8
 #pragma unroll
-    for (uint32_t j = 3; j < 9; ++j) bs[j] = __builtin_bswap32(frame_dw(lds, hw, g, sa, j));
+    for (uint32_t j = 3; j < 9; ++j) bs[j] = __builtin_bswap32(frame_dw(lds, hw, g, sa, j, xo));
     const uint32_t etype = bs[3] >> 16;                                       // headers.go:209-215
     const uint32_t vihl = (bs[3] >> 8) & 0xffu;
     {   // eth/headers.go:333-340 via Put (:289-301): version forced to 4, checksum zeroed, 20 bytes.
@@ -468,7 +474,7 @@ __device__ __forceinline__ Parsed parse_frame(const char* lds, uint32_t hw, uint
     uint32_t lb[6];
 #pragma unroll
     for (uint32_t i = 0; i < 6; ++i)
-        lb[i] = __builtin_bswap32(frame_dw_t<kSlotDw>(lds, hw, g, sa, q + i, fb, ((sa + len + 3u) >> 2) - 1u));
+        lb[i] = __builtin_bswap32(frame_dw_t<kSlotDw>(lds, hw, g, sa, q + i, fb, ((sa + len + 3u) >> 2) - 1u, xo));
     const uint32_t sport = lb[0] & 0xffffu, dport = lb[1] >> 16;
     uint32_t lenword;
     if (proto == 17u) {                                                       // :222-244
@@ -558,29 +564,32 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, ui
 // end in a vmcnt(0) that drains the row ring).
 template <uint32_t kOps, int kSlotDw = kHdrDwords>
 __device__ __forceinline__ void parse_tile_body(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
-                                                uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk) {
+                                                uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk,
+                                                uint32_t xo = 0u) {
     const char* lds = g_lds;
-    const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3));
+    const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3, xo));
     const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
-    const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 4)) >> 16;
+    const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 4, xo)) >> 16;
     const uint32_t end = (14u + tl) & 0xffffu;
     // [0, off) spans at most 3 + 74 bytes: absolute dwords < 20 (a 16-dword slot holds [0, 64 - sa);
     // longer IP headers are summed from global memory)
     const uint32_t h1 = min(off, len);
-    uint32_t hsum = slot_sum(lds, hw, grp, gl, sa, 0, (int)h1, min(5, kSlotDw / 4));
+    uint32_t hsum = slot_sum(lds, hw, grp, gl, sa, 0, (int)h1, min(5, kSlotDw / 4), xo);
     if (kSlotDw < 32 && sa + h1 > 4u * kSlotDw) hsum = global_sum(fbs, sa, 0, (int)h1);
     const bool pad_in_slot = sa + len <= 4u * kSlotDw;
     int64_t pad = -1;
     if (__ballot(len >= 34u && end < len && pad_in_slot) != 0) {
-        const uint32_t ps = slot_sum(lds, hw, grp, gl, sa, (int)min(end, len), (int)len, kSlotDw / 4);
+        const uint32_t ps = slot_sum(lds, hw, grp, gl, sa, (int)min(end, len), (int)len, kSlotDw / 4, xo);
         if (pad_in_slot) pad = (int64_t)ps;
     }
-    if (parser) park_parsed<kOps>(g_lds, pk, grp, parse_frame<kOps, kSlotDw>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs));
+    if (parser)
+        park_parsed<kOps>(g_lds, pk, grp, parse_frame<kOps, kSlotDw>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs, xo));
 }
 template <uint32_t kOps, int kSlotDw = kHdrDwords>
 __device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
-                                                     uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk) {
-    parse_tile_body<kOps, kSlotDw>(hw, grp, gl, sa, len, mtu, fbs, parser, pk);
+                                                     uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk,
+                                                     uint32_t xo = 0u) {
+    parse_tile_body<kOps, kSlotDw>(hw, grp, gl, sa, len, mtu, fbs, parser, pk, xo);
 }
 
 // Final L4 checksum + verdict (parser lane) once the streamed sum is known.
@@ -931,6 +940,8 @@ struct TileA {
     int P;      // wave-uniform: rows of the tile (a multiple of kPrefetch; 0 = no rows)
     int H;      // wave-uniform: leading rows that take the masked path
     uint32_t ph;  // block-aligned rows: absolute 64-B block phase (in dwords) of frame dword 0
+    int r0f;      // block-aligned rows: the row of the frame's first block (large for an empty group)
+    int cap;      // wave-uniform: every frame's first 3 blocks lie in the first block of rows (captured there)
     // derived per use (they would otherwise hold VGPRs across the row loop)
     __device__ __forceinline__ uint32_t sa() const { return (uint32_t)S & 3u; }
     // block-aligned rows: dwords past the frame end in its last row (the row ends on a 64-B block)
@@ -966,6 +977,8 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     const int rows = kAl ? (int)((T.ph + (uint32_t)ndb) >> 4) * (nd > 0) : (nd + kRowDwords - 1) / kRowDwords;
     const int R = group_max(rows);
     T.P = (R + kRingA<kAl> - 1) / kRingA<kAl> * kRingA<kAl>;
+    T.r0f = nd > 0 ? T.P - rows : (1 << 20);
+    T.cap = __ballot(nd > 0 && min(T.r0f + 3, T.P) > kRingA<kAl>) == 0;
     uint64_t ld_sdw = T.sdw();
     int ld_nd = ndb;
     uint32_t ld_ph = T.ph;
@@ -1198,15 +1211,41 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     // the other groups stay empty)
     fpt = __builtin_amdgcn_readfirstlane(fpt);
     const uint32_t ntiles = (n + fpt - 1) / fpt;
-    const uint32_t hw = kLdsHdr + wave * kHdrWaveBytes;  // this wave's header slots
+    // Header slots captured from the rows (block-aligned rows, FS_HDR_CAPTURE): the first block
+    // of rows holds every frame's first 3 blocks (checked per tile: T.cap), and each of those
+    // rows is written to the slot as it is consumed -- cell 4k + gl of the slot holds the lane's
+    // 16 B of the frame's block k, so slot dword s is frame dword s - ph (the parse's `xo`).
+    // No header DMA: its 2 KB per wave were 0.5 us of the preamble's vector-memory burst. 3 KB
+    // per wave (12 cells), overlapping the wave scratch the one-pass kernel leaves unused.
+    constexpr bool kCapture = kAl && FS_HDR_CAPTURE;
+    constexpr uint32_t kHwStride = kCapture ? 3072u : kHdrWaveBytes;
+    static_assert(kLdsHdr + kWavesPerBlock * 3072u <= kLdsBytes, "captured header slots fit");
+    const uint32_t hw = kLdsHdr + wave * kHwStride;  // this wave's header slots
     // where the parse is parked until the finish: the header slot itself, or with chained tiles
     // (the next tile's header DMA lands before this tile's finish) the wave's scratch area,
     // which the one-pass kernel does not otherwise use
-    constexpr bool kChain = kAl && FS_CHAIN;
+    constexpr bool kChain = kAl && FS_CHAIN && !kCapture;
     const uint32_t pk = kChain ? kLdsWave + wave * kWaveScratchBytes : hw;
     // where a masked row's chunk is loaded (block-aligned rows: where it lies, or wholly before
     // the frame's first block, the lane's chunk of that block)
     auto lpos = [&](int rel, int lo) -> int { return kAl ? (rel >= lo ? rel : lo + 4 * (int)gl) : load_pos(rel, lo); };
+    // the tile's header slots: by LDS-DMA, or (capture mode) from the first block of rows, or for
+    // a tile whose frames start too late for that, by plain loads here (rare: mixed lengths)
+    auto tile_header = [&](const TileA& Tt) -> bool {
+        if (!kCapture) return header_dma<true, kSlotA>(Tt, frames, lds, hw, gl, lane);
+        if (!Tt.cap) {
+            const int rows = Tt.P - Tt.r0f;
+            const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + (Tt.sdw() << 2));
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if (Tt.len >= 4u && k < rows) {
+                    const u32x4 v = load_row(fb, -(int)Tt.ph + 16 * k + 4 * (int)gl);
+                    *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)(4 * k + (int)gl) * 256u + grp * 16u) = v;
+                }
+            }
+        }
+        return false;
+    };
 
     LaneKeys keys;
     {
@@ -1262,12 +1301,17 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     };
     // (FS_ROWS_FIRST: the first rows before the header DMA -- still older than the first
     // block's refills, which is all the parse's vmcnt(kPfA) needs; measured within noise)
-    if (FS_ROWS_FIRST) first_rows();
-    if (first) x4 = header_dma<true, kSlotA>(T, frames, lds, hw, gl, lane);
+    if (FS_ROWS_FIRST || kCapture) first_rows();
+    if (first) x4 = tile_header(T);
     FS_STAMP(13);
-    if (!FS_ROWS_FIRST) first_rows();
+    if (!FS_ROWS_FIRST && !kCapture) first_rows();
     FS_STAMP(9);
-    tables_landed<kPfA, kSlotA>(first, T.P > 0, x4);
+    if (kCapture) {  // no header DMA: the table pieces are older than the rows
+        if (first && T.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
+        else __builtin_amdgcn_s_waitcnt(0x0070);
+    } else {
+        tables_landed<kPfA, kSlotA>(first, T.P > 0, x4);
+    }
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -1302,10 +1346,12 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         // The header DMA was issued before the tile's rows; vmcnt(kPfA) retires it once the
         // first block's refills are the only younger loads.
         auto parse = [&](bool refilled) {
-            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
-            else __builtin_amdgcn_s_waitcnt(0x0070);
+            if (!kCapture) {  // the DMA'd slot (captured slots are this wave's own LDS writes)
+                if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
+                else __builtin_amdgcn_s_waitcnt(0x0070);
+            }
             parse_tile<kOps, kSlotA>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
-                       parser, pk);
+                       parser, pk, kCapture ? T.ph : 0u);
             if (FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             if (chain) tile_descriptors(tnext, grp, n, offsets, lengths, Sn, lenn, fpt);
         };
@@ -1338,6 +1384,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 else if (masked) masked_row(lds, keys, pf[i], rel, load_pos(rel, T.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
                 else if (kAl && !kRefill && i == kPfA - 1) tail_row_al(lds, keys, pf[i], rel, T.nd(), T.tail_mask(), A, cs);
                 else lean_row(lds, keys, pf[i], A, cs);
+                if (kCapture && r0 == 0 && T.cap) {  // the frame's blocks 0..2 into the header slot
+                    const uint32_t k = (uint32_t)(i - T.r0f);
+                    if (k < 3u) *reinterpret_cast<u32x4*>(lds + hw + (4u * k + gl) * 256u + grp * 16u) = pf[i];
+                }
                 if (kRefill) {
                     const int rn = rel + kRowDwords * kPfA;
                     pf[i] = load_row(T.gfb, r + kPfA < T.H ? lpos(rn, T.lo) : rn);
@@ -1466,7 +1516,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             descriptors_ready<kOps>(S, len);
             tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
             if (!FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
-            header_dma<true, kSlotA>(T, frames, lds, hw, gl, lane);
+            if (!kCapture) tile_header(T);
             if (T.P > 0) {
 #pragma unroll
                 for (int i = 0; i < kPfA; ++i) {
@@ -1474,6 +1524,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                     pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
                 }
             }
+            if (kCapture) tile_header(T);
         }
     }
 }
