@@ -81,6 +81,10 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_LATE_REPORT
 #define FS_LATE_REPORT 0  // one-pass kernel: the mixed-length report after the parse (measured slower)
 #endif
+#ifndef FS_EARLY_BARRIER
+#define FS_EARLY_BARRIER 0  // one-pass kernel: the tables barrier right after the descriptors, before the geometry
+                           // and the first rows (measured 1.4 us slower on C2)
+#endif
 #ifndef FS_HDR_CAPTURE
 #define FS_HDR_CAPTURE 1  // block-aligned one-pass kernel: header slots captured from the first rows (no header DMA)
 #endif
@@ -1280,6 +1284,13 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         FS_STAMP(7);
         descriptors_ready<kOps>(S, len);
         FS_STAMP(8);
+        if (FS_EARLY_BARRIER) {
+            // the tables are ready here: the descriptors' vmcnt(0) also retired the table pieces
+            // (issued before them), lgkmcnt(0) this wave's region-A stores; the geometry and the
+            // first rows follow the barrier, so no wave waits for another's row issue
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+        }
         T.P = 0;
         if (first) {
             tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
@@ -1306,14 +1317,16 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     FS_STAMP(13);
     if (!FS_ROWS_FIRST && !kCapture) first_rows();
     FS_STAMP(9);
-    if (kCapture) {  // no header DMA: the table pieces are older than the rows
+    if (FS_EARLY_BARRIER) {
+        // (the tables were ready at the early barrier)
+    } else if (kCapture) {  // no header DMA: the table pieces are older than the rows
         if (first && T.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
         else __builtin_amdgcn_s_waitcnt(0x0070);
     } else {
         tables_landed<kPfA, kSlotA>(first, T.P > 0, x4);
     }
     FS_STAMP(10);
-    __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    if (!FS_EARLY_BARRIER) __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(0);
     if (FS_AGE_PRIO) {  // the SIMD's younger waves (wave >> 2: its 4 waves in launch order) outrank the older
         const uint32_t w = __builtin_amdgcn_readfirstlane(wave) >> 2;
