@@ -100,7 +100,8 @@ func (g *GPU) Close() error {
 func (g *GPU) lastErr() error { return errors.New("framesum: " + C.GoString(C.fs_last_error(g.ctx))) }
 
 // stage packs frames back to back, each at a 4-byte aligned offset, into pinned memory,
-// followed by 16 spare bytes (the engine may read up to 3 bytes past a frame's end). The
+// followed by 16 spare bytes (slack for the dword-rounded copy span; on the device the engine
+// reads the 64-byte blocks around each frame inside its own staging buffer). The
 // copies run on the host; the device reads the pinned buffer over PCIe in chunks that
 // overlap its kernels (fs_digest_batch_host).
 func (g *GPU) stage(frames [][]byte, spare int) ([]byte, error) {
