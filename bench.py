@@ -66,13 +66,14 @@ def parse():
                         "append in place (fs_fill_batch); fcs: RX of wire frames carrying an FCS")
     p.add_argument("--min-warm", type=int, default=500,
                    help="device pre-warm: when --warmup is below this, (min-warm - warmup) extra untimed "
-                        "launches run first, on the main stream, without the gather (reported as prewarm_launches)")
+                        "launches run first, over the streams, without the gather (reported as prewarm_launches)")
     p.add_argument("--kernel", type=int, default=0,
-                   help="fs_ctx_set_kernel variant: 0 automatic (the 16-lane kernel), 1 / 2 the 4-lane one-pass / "
-                        "mixed-length kernels, 3 the 16-lane kernel")
-    p.add_argument("--streams", type=int, default=4,
+                   help="fs_ctx_set_kernel variant: 0 automatic, 1 one-pass (end-anchored rows), 2 mixed-length, "
+                        "3 16-lane, 4 one-pass (block-aligned rows)")
+    p.add_argument("--streams", type=int, default=5,
                    help="HIP streams the steps rotate over: step i+1's kernel starts on the CUs step i's "
-                        "tail frees (every batch is still fully digested)")
+                        "tail frees (every batch is still fully digested). 5 measured best on the 4 hardware "
+                        "queues of the box (DESIGN.md §5.1)")
     return p.parse_args()
 
 
@@ -286,7 +287,9 @@ def main():
     prewarm = max(0, args.min_warm - args.warmup)
     for i in range(prewarm):
         fb, fo, fl = batches[i % nb]
-        run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=main_stream)
+        # over every stream (slot k on stream k): a stream's first launch costs hundreds of us,
+        # which must not land in the timed region when --warmup is below the stream count
+        run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=streams[i % ns])
     torch.cuda.synchronize()
     for i in range(args.warmup):
         step(i)
