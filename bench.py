@@ -244,7 +244,12 @@ def main():
         gviews = [[[views(gbuf[st][g], j) for j in range(G)] for g in range(2)] for st in range(ns)]
         recv = [[[torch.empty_like(gbuf[st][g]) for _ in range(world)] if rank == 0 else None for g in range(2)]
                 for st in range(ns)]
+        # the final partial groups of all streams are packed here (only their written slabs) and
+        # go to rank 0 in ONE gather: a short timed region ends with partial groups only
+        stage = torch.empty(ns * G * slab, dtype=torch.uint8, device=dev)
+        recv_stage = [torch.empty_like(stage) for _ in range(world)] if rank == 0 else None
         pend = [[None, None] for _ in range(ns)]  # per stream and group: the RCCL work of its latest gather
+        last = {}  # (stream, group) -> ("own" | "all", slabs): which gather delivered it last
     flat = torch.empty(nslot * slab, dtype=torch.uint8, device=dev)
     outs, stats = zip(*[views(flat, k) for k in range(nslot)])
 
@@ -265,17 +270,38 @@ def main():
             run_op(fb, fo, fl, mtu=0, out=o, status=st, stream=s)
             if j == G - 1:
                 pend[si][g] = dist.gather(gbuf[si][g], recv[si][g], dst=0, async_op=True)
+                last[(si, g)] = ("own", G)
 
     def drain(i_end: int):
         if not gather:
             return
         # partly filled groups still go to rank 0 (same calls on every rank: i_end is common)
+        part = []
         for si in range(ns):
             q_end = (i_end - si + ns - 1) // ns  # steps this stream ran
             g = (q_end // G) % 2
             if q_end % G != 0 and pend[si][g] is None:
+                part.append((si, g, q_end % G))  # (stream, group, slabs written in it)
+        if len(part) == ns and len({g for _, g, _ in part}) == 1:
+            # every stream ends in the same partial group: its written slabs, packed on the main
+            # stream once that has joined the others, go to rank 0 in one gather
+            g, m = part[0][1], max(k for _, _, k in part)
+            for si in range(1, ns):
+                streams[0].wait_stream(streams[si])
+            with torch.cuda.stream(streams[0]):
+                for si in range(ns):
+                    stage[si * m * slab : (si + 1) * m * slab].copy_(gbuf[si][g][: m * slab])
+                rv = [r[: ns * m * slab] for r in recv_stage] if rank == 0 else None
+                work = dist.gather(stage[: ns * m * slab], rv, dst=0, async_op=True)
+            for si in range(ns):
+                pend[si][g] = work
+                last[(si, g)] = ("all", m)
+        else:
+            for si, g, k in part:
                 with torch.cuda.stream(streams[si]):
-                    pend[si][g] = dist.gather(gbuf[si][g], recv[si][g], dst=0, async_op=True)
+                    rv = [r[: k * slab] for r in recv[si][g]] if rank == 0 else None
+                    pend[si][g] = dist.gather(gbuf[si][g][: k * slab], rv, dst=0, async_op=True)
+                last[(si, g)] = ("own", k)
         for si in range(ns):
             for g in range(2):
                 if pend[si][g] is not None:
@@ -316,9 +342,9 @@ def main():
     if gather and rank == 0:
         # every group's latest gather delivered rank 0's own slabs intact (a check of the loop)
         torch.cuda.synchronize()
-        for si in range(ns):
-            for g in range(2):
-                assert torch.equal(recv[si][g][0], gbuf[si][g]), "gathered digests differ from rank 0's own"
+        for (si, g), (how, m) in last.items():
+            got = recv[si][g][0][: m * slab] if how == "own" else recv_stage[0][si * m * slab : (si + 1) * m * slab]
+            assert torch.equal(got, gbuf[si][g][: m * slab]), "gathered digests differ from rank 0's own"
 
     # ---- kernel-only timing with HIP events on the launch stream (roofline.achieved): one event
     # pair around K back-to-back launches on one stream (no overlap with another launch), so the
