@@ -222,8 +222,9 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
  * the next launch picks accordingly (the one-pass choice reads each frame as the
  * 64-byte blocks that hold it). 1 forces the one-pass kernel with rows anchored at
  * the frame end, 2 the mixed one, 3 the 16-lane kernel (256-byte rows per frame;
- * DESIGN.md §3.8), 4 the one-pass kernel with block-aligned rows. Results are
- * identical in every case; only the speed differs. */
+ * DESIGN.md §3.8), 4 the one-pass kernel with block-aligned rows, 5 the same as
+ * two 8-wave workgroups per CU (digest and FCS verify; the TX fill runs 4). Results
+ * are identical in every case; only the speed differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
 /* Pinned host memory helpers for fs_digest_batch_host callers. */

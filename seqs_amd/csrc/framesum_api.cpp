@@ -490,7 +490,7 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
     ctx->err.clear();
-    if (variant < 0 || variant > 4) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0..4");
+    if (variant < 0 || variant > 5) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0..5");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
 }

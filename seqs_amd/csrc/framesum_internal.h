@@ -16,8 +16,10 @@ namespace framesum {
 struct FsTables {
     // Region A (64 KB): 256 entry rows x 64 dword slots. Slot 8*b + c (c = 0..7) holds
     // Z_64[b][e] (one 64-byte frame-row of stream stride); the 8 copies make the kernel's
-    // lookups LDS-bank-conflict-free. Slots 32..63 are unused (the 256-B entry stride lets
-    // one v_perm_b32 form the address).
+    // lookups LDS-bank-conflict-free (the 256-B entry stride lets one v_perm_b32 form the
+    // address). Slots 32..63 hold 8 plain tables for the two-workgroups-per-CU kernel, which
+    // copies region A as it is: slot 32 + ((4 t + b) ^ (e & 31)) = T_t[b][e] for the tables
+    // kA2Tables (the XOR spreads one table's entries over the banks as a plain [4][256] table's).
     uint32_t region_a[256][64];
     uint32_t z32[4][256];      // Z_32 : lane-tree level 1 (lanes l, l+2)
     uint32_t z16[4][256];      // Z_16 : lane-tree level 2 (lanes l, l+1)
@@ -31,6 +33,8 @@ struct FsTables {
     uint32_t z64_basis[4][8];  // Z_64[b][1 << j]: region A's entries are XORs of these
 };
 constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 10;  // the LDS image: everything before z64_basis
+// region A's plain tables (slots 32..63): the zero shift in bytes of table t = 0..7
+constexpr int kA2Tables[8] = {4, 8, 12, 16, 32, 48, 2, 1};
 static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout");
 
 void build_tables(FsTables* t);
@@ -70,6 +74,7 @@ void build_tables_w(FsTablesW* t);
 // checksums written into the frames and/or the FCS appended after them); or the RX digest of
 // wire frames whose lengths include a trailing FCS.
 enum class FsOp { kDigest, kFill, kFcs };
+// force 5 = the same kernel as two 8-wave workgroups per CU (LayA2: RX ops; the fill runs force 4's);
 // force 4 = the one-pass kernel with block-aligned rows (what force 0 uses for the one-pass choice;
 // force 1 keeps the end-anchored rows).
 // `tables_w`: the 16-lane kernel's tables; force 3 = the 16-lane kernel (an experimental variant,

@@ -185,6 +185,24 @@ constexpr uint32_t kLdsAlloc = kLdsBytes > kW_LdsBytes ? kLdsBytes : kW_LdsBytes
 // out-of-line parse routine addresses it as LDS (ds_read), not through a flat pointer.
 __shared__ __attribute__((aligned(16))) char g_lds[kLdsAlloc];
 
+// ---- LDS map of the two-workgroups-per-CU kernel (digest_kernel_a with LayA2): 8 waves and
+// 80 KB per workgroup, so that a CU holds two and a launch's workgroups start while the previous
+// launch's still stream. [0, 64 KB): FsTables::region_a as it is, by LDS-DMA -- each 256-B entry
+// row holds Z64's 8 replicated copies (bytes 0..127, the row lookups' conflict-free layout) and,
+// in bytes 128..255, the 8 plain tables the combine and the finish use, XOR-swizzled by the entry
+// (kA2Plain); [64 KB, 80 KB): 8 captured header slots of 2 KB (the frame's first 2 blocks).
+constexpr int kA2Waves = 8;
+constexpr uint32_t kA2Hdr = 65536;
+constexpr uint32_t kA2HdrStride = 2048;
+constexpr uint32_t kA2Bytes = kA2Hdr + kA2Waves * kA2HdrStride;
+static_assert(kA2Bytes == 80u * 1024u, "two workgroups per CU");
+__shared__ __attribute__((aligned(16))) char g_lds2[kA2Bytes];
+template <bool kL2>
+__device__ __forceinline__ char* lds_image() {
+    if constexpr (kL2) return g_lds2;
+    else return g_lds;
+}
+
 #ifdef FS_STAMPS
 // Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
 __device__ unsigned long long g_fs_stamps[8192 * 16];
@@ -339,6 +357,7 @@ __device__ __forceinline__ void masked_row(const char* lds, const LaneKeys& k, u
 // wholly before the frame, somewhere irrelevant), so no realignment. Dwords at or past the frame
 // end (only in the last row) leave the stream untouched: the combine then shifts that stream
 // by its distance to the frame end, which the skipped update would have overshot.
+template <uint32_t kRegion = kLdsRegionA>
 __device__ __forceinline__ void masked_row_al(const char* lds, const LaneKeys& k, u32x4 u, int rel, int nd,
                                               uint32_t sa, uint32_t tail_mask, uint32_t (&A)[4], uint32_t& cs) {
     const uint32_t head_mask = 0xffffffffu << (8u * sa);
@@ -352,12 +371,13 @@ __device__ __forceinline__ void masked_row_al(const char* lds, const LaneKeys& k
         if (x == 1) c = ~head_mask;
         if (x == nd - 1) d &= tail_mask;
         const bool in = x < nd;
-        const uint32_t a = zrep(lds, A[j], k, d ^ c);
+        const uint32_t a = zrep<kRegion>(lds, A[j], k, d ^ c);
         A[j] = in ? a : A[j];
         cs = sad16(in ? d : 0u, cs);
     }
 }
 // The last row of block-aligned rows when it is otherwise lean.
+template <uint32_t kRegion = kLdsRegionA>
 __device__ __forceinline__ void tail_row_al(const char* lds, const LaneKeys& k, u32x4 u, int rel, int nd,
                                             uint32_t tail_mask, uint32_t (&A)[4], uint32_t& cs) {
     const uint32_t v[4] = {u.x, u.y, u.z, u.w};
@@ -366,7 +386,7 @@ __device__ __forceinline__ void tail_row_al(const char* lds, const LaneKeys& k, 
         const int x = rel + j;
         const uint32_t d = (x == nd - 1) ? (v[j] & tail_mask) : v[j];
         const bool in = x < nd;
-        const uint32_t a = zrep(lds, A[j], k, d);
+        const uint32_t a = zrep<kRegion>(lds, A[j], k, d);
         A[j] = in ? a : A[j];
         cs = sad16(in ? d : 0u, cs);
     }
@@ -566,11 +586,11 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, ui
 // `pk`: where the parse result is parked (the 4-lane kernels park it in the header slot itself).
 // parse_tile_body: the same, inlined (the 16-lane kernel's single parse site: a call there would
 // end in a vmcnt(0) that drains the row ring).
-template <uint32_t kOps, int kSlotDw = kHdrDwords>
+template <uint32_t kOps, int kSlotDw = kHdrDwords, bool kL2 = false>
 __device__ __forceinline__ void parse_tile_body(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
                                                 uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk,
                                                 uint32_t xo = 0u) {
-    const char* lds = g_lds;
+    const char* lds = lds_image<kL2>();
     const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3, xo));
     const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
     const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 4, xo)) >> 16;
@@ -587,13 +607,13 @@ __device__ __forceinline__ void parse_tile_body(uint32_t hw, uint32_t grp, uint3
         if (pad_in_slot) pad = (int64_t)ps;
     }
     if (parser)
-        park_parsed<kOps>(g_lds, pk, grp, parse_frame<kOps, kSlotDw>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs, xo));
+        park_parsed<kOps>(lds_image<kL2>(), pk, grp, parse_frame<kOps, kSlotDw>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs, xo));
 }
-template <uint32_t kOps, int kSlotDw = kHdrDwords>
+template <uint32_t kOps, int kSlotDw = kHdrDwords, bool kL2 = false>
 __device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
                                                      uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk,
                                                      uint32_t xo = 0u) {
-    parse_tile_body<kOps, kSlotDw>(hw, grp, gl, sa, len, mtu, fbs, parser, pk, xo);
+    parse_tile_body<kOps, kSlotDw, kL2>(hw, grp, gl, sa, len, mtu, fbs, parser, pk, xo);
 }
 
 // Final L4 checksum + verdict (parser lane) once the streamed sum is known.
@@ -646,6 +666,12 @@ __device__ __forceinline__ void st8(uint8_t* p, uint32_t v) { *p = (uint8_t)v; }
 struct LayoutA {
     static constexpr uint32_t kZfin = kLdsZfin;
     __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift(lds, v, k); }
+    // Z_(4-t)(v): the final step (t = bytes of dword rounding)
+    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
+        return zplain(lds, v, kZfin + 4096u * t);
+    }
+    // the standard CRC-32 byte table (Z_1's byte table 0)
+    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) { return lds32(lds, kZfin + 3u * 4096u + (i << 2)); }
 };
 
 template <uint32_t kOps, class L = LayoutA>
@@ -665,15 +691,15 @@ __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, u
         uint32_t c = 0xffffffffu;
         const uint8_t* fbytes = frames + S;
         for (uint32_t p = 0; p < len; ++p)
-            c = lds32(lds, L::kZfin + 3u * 4096u + (((c ^ fbytes[p]) & 0xffu) << 2)) ^ (c >> 8);
+            c = L::byte1(lds, (c ^ fbytes[p]) & 0xffu) ^ (c >> 8);
         crcv = ~c;
     } else {
         const uint32_t tpad = (4u - te) & 3u;  // zero bytes appended by the dword rounding
-        crcv = ~zplain(lds, Y, L::kZfin + 4096u * tpad);
+        crcv = ~L::fin(lds, Y, tpad);
     }
     uint32_t verdict = P.verdict, l4 = 0u;
     if (P.compute) l4 = finish_l4(fbs, sa, len, P, cs, verdict);
-    if (kOps == kOpsTx) {
+    if constexpr (kOps == kOpsTx) {
         uint8_t* wf = wframes + S;
         if ((tx & kTxFill) && P.compute) {
             // write the IPv4 checksum at [24, 26) and the L4 checksum at its field, big-endian;
@@ -945,7 +971,7 @@ struct TileA {
     int H;      // wave-uniform: leading rows that take the masked path
     uint32_t ph;  // block-aligned rows: absolute 64-B block phase (in dwords) of frame dword 0
     int r0f;      // block-aligned rows: the row of the frame's first block (large for an empty group)
-    int cap;      // wave-uniform: every frame's first 3 blocks lie in the first block of rows (captured there)
+    int cap;      // wave-uniform: every frame's first 3 (LayA2: 2) blocks lie in the first block of rows (captured there)
     // derived per use (they would otherwise hold VGPRs across the row loop)
     __device__ __forceinline__ uint32_t sa() const { return (uint32_t)S & 3u; }
     // block-aligned rows: dwords past the frame end in its last row (the row ends on a 64-B block)
@@ -969,7 +995,7 @@ struct TileA {
 // it, the last one ending on the block boundary after the frame end (nd + ealign() dwords from
 // frame dword 0), so a row load never straddles a line; the end-anchored rows otherwise
 // (ending at the frame's dword-rounded end).
-template <bool kAl>
+template <bool kAl, int kCapBlocks = 3>
 __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
                                               uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
                                               uint32_t fpt) {
@@ -982,7 +1008,7 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     const int R = group_max(rows);
     T.P = (R + kRingA<kAl> - 1) / kRingA<kAl> * kRingA<kAl>;
     T.r0f = nd > 0 ? T.P - rows : (1 << 20);
-    T.cap = __ballot(nd > 0 && min(T.r0f + 3, T.P) > kRingA<kAl>) == 0;
+    T.cap = __ballot(nd > 0 && min(T.r0f + kCapBlocks, T.P) > kRingA<kAl>) == 0;
     uint64_t ld_sdw = T.sdw();
     int ld_nd = ndb;
     uint32_t ld_ph = T.ph;
@@ -1060,7 +1086,6 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
     dst[0] = u32x4{v, v, v, v};
     dst[1] = u32x4{v, v, v, v};
 }
-
 // LDS-DMA by inline asm: invisible to hipcc's vmcnt model (the builtin makes it drain later
 // LDS reads with vmcnt(0)); unknown VMEM ops only make the compiler's own counted waits
 // stricter (loads retire in order). Every use is covered by an explicit counted wait.
@@ -1174,6 +1199,72 @@ __device__ __forceinline__ void combine_piece(const char* lds, uint32_t gl, cons
     csum = cs;
 }
 
+// The one-pass kernel's LDS layouts. LayA1: one 16-wave workgroup per CU (region A built in
+// place, the plain tables by LDS-DMA, 3-block header slots). LayA2: two 8-wave workgroups per CU
+// (kA2* map above: region A and the plain tables in one 64-KB LDS-DMA image, 2-block header
+// slots; block-aligned RX kernels only -- the TX fill's long CRC shifts need Z768).
+struct LayA1 : LayoutA {
+    static constexpr int kWaves = kWavesPerBlock;
+    static constexpr bool kL2 = false;
+    static constexpr uint32_t kRegion = kLdsRegionA;
+    static constexpr uint32_t kHdr = kLdsHdr;
+    static constexpr uint32_t kCapStride = 3072;
+    static constexpr int kCapBlocks = 3;
+    static constexpr int kSlotAl = FS_HDR_AL;
+    // the combine's shifts Z_(4c), c = 1..3, and Z_(16a), a = 1..3
+    __device__ static __forceinline__ uint32_t z4c(const char* lds, uint32_t v, uint32_t c) {
+        return zplain(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
+    }
+    __device__ static __forceinline__ uint32_t z16a(const char* lds, uint32_t v, uint32_t a) {
+        return zplain(lds, v, a == 1u ? kLdsZ16 : a == 2u ? kLdsZ32 : kLdsZ48);
+    }
+};
+struct LayA2 {
+    static constexpr int kWaves = kA2Waves;
+    static constexpr bool kL2 = true;
+    static constexpr uint32_t kRegion = 0;
+    static constexpr uint32_t kHdr = kA2Hdr;
+    static constexpr uint32_t kCapStride = kA2HdrStride;
+    static constexpr int kCapBlocks = 2;
+    // the captured slot holds frame dwords [0, 32 - ph) with ph <= 15: the parse treats it as a
+    // 16-dword slot (frame_dw_t / slot_sum read what lies past it from global memory)
+    static constexpr int kSlotAl = 16;
+    // plain table t (kA2Tables: Z4 Z8 Z12 Z16 Z32 Z48 Z2 Z1) in region A's upper half, swizzled
+    __device__ static __forceinline__ uint32_t zt(const char* lds, uint32_t v, uint32_t t) {
+        uint32_t r = 0u;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t e = (v >> (8u * b)) & 0xffu;
+            r ^= lds32(lds, (e << 8) + 128u + (((4u * t + b) ^ (e & 31u)) << 2));
+        }
+        return r;
+    }
+    __device__ static __forceinline__ uint32_t z4c(const char* lds, uint32_t v, uint32_t c) { return zt(lds, v, c - 1u); }
+    __device__ static __forceinline__ uint32_t z16a(const char* lds, uint32_t v, uint32_t a) { return zt(lds, v, a + 2u); }
+    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
+        if (t == 1u) v = zt(lds, v, 6u);  // Z3 = Z1 Z2
+        return zt(lds, v, t == 0u ? 0u : t == 2u ? 6u : 7u);
+    }
+    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) {
+        return lds32(lds, (i << 8) + 128u + ((28u ^ (i & 31u)) << 2));
+    }
+};
+
+// LayA2's tables: region A's 64 KB as FsTables holds it (Z64's copies and the plain tables), 8
+// pieces of 1 KB per wave. (Building the Z64 half in place and copying only the plain tables'
+// 32 KB, lane-masked, measured 2-3% slower: the basis loads wait behind the DMAs.)
+__device__ __forceinline__ void a2_tables_dma(const FsTables* __restrict__ tabs, const char* lds, uint32_t wave,
+                                              uint32_t lane) {
+    const uint32_t lds0 = lds_base(lds);
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+    for (uint32_t k = 0; k < ((FS_DIAG & 2) ? 0u : 65536u / 1024u / kA2Waves); ++k) {
+        const uint32_t c = w0 + k * kA2Waves;
+        dma_x4(reinterpret_cast<const char*>(tabs->region_a) + c * 1024u + lane * 16u,
+               __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
+    }
+}
+
 // `report` = the host-mapped report word's address in bits 0..47, the launch id in bits 48..63
 // (one kernel argument, loaded where it is used: nothing of it stays live through the tile loop).
 __device__ __forceinline__ void post_report(uint64_t report) {
@@ -1185,32 +1276,34 @@ __device__ __forceinline__ void post_report(uint64_t report) {
 // `report` whether any tile would have run better in mode B, so that the host launches
 // digest_kernel_ab next time (launch_digest).
 // The wave's first tile (later tiles: + all waves). Every map is a bijection on [0, nwaves).
+template <int kW = kWavesPerBlock>
 __device__ __forceinline__ uint32_t first_tile(uint32_t wave) {
     if (FS_TILE_MAP == 1) return wave * gridDim.x + blockIdx.x;
     if (FS_TILE_MAP == 2 && (gridDim.x & 7u) == 0u) {  // workgroup b runs on XCD b % 8
         const uint32_t per = gridDim.x >> 3;
-        return ((blockIdx.x & 7u) * per + (blockIdx.x >> 3)) * kWavesPerBlock + wave;
+        return ((blockIdx.x & 7u) * per + (blockIdx.x >> 3)) * kW + wave;
     }
-    return blockIdx.x * kWavesPerBlock + wave;
+    return blockIdx.x * kW + wave;
 }
 
-template <uint32_t kOps, bool kAl>
-__global__ void __launch_bounds__(kThreads, 1)
+template <uint32_t kOps, bool kAl, class Lay = LayA1>
+__global__ void __launch_bounds__(Lay::kWaves * kWave, 1)
 digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
                 const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx, uint32_t fpt) {
-    char* lds = g_lds;
+    static_assert(!Lay::kL2 || (kAl && FS_HDR_CAPTURE && kOps != kOpsTx), "LayA2: block-aligned RX kernels with header capture");
+    char* lds = lds_image<Lay::kL2>();
     constexpr int kPfA = kRingA<kAl>;
     // header slot dwords (FS_HDR_AL = 16 with block-aligned rows: one dwordx4 DMA per wave, the
     // parse reading the rare bytes past the slot from global memory; measured within noise of 32)
-    constexpr int kSlotA = kAl ? FS_HDR_AL : kHdrDwords;
+    constexpr int kSlotA = kAl ? Lay::kSlotAl : kHdrDwords;
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t grp = lane >> 2;   // frame slot of this lane's group
     const uint32_t gl = lane & 3u;    // lane within the group
-    const uint32_t gwave = first_tile(wave);
-    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+    const uint32_t gwave = first_tile<Lay::kWaves>(wave);
+    const uint32_t nwaves = gridDim.x * Lay::kWaves;
     // fpt: frames per tile (16, or 8 / 4 for batches too small to give every wave a tile;
     // the other groups stay empty)
     fpt = __builtin_amdgcn_readfirstlane(fpt);
@@ -1222,9 +1315,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     // No header DMA: its 2 KB per wave were 0.5 us of the preamble's vector-memory burst. 3 KB
     // per wave (12 cells), overlapping the wave scratch the one-pass kernel leaves unused.
     constexpr bool kCapture = kAl && FS_HDR_CAPTURE;
-    constexpr uint32_t kHwStride = kCapture ? 3072u : kHdrWaveBytes;
-    static_assert(kLdsHdr + kWavesPerBlock * 3072u <= kLdsBytes, "captured header slots fit");
-    const uint32_t hw = kLdsHdr + wave * kHwStride;  // this wave's header slots
+    constexpr uint32_t kHwStride = kCapture ? Lay::kCapStride : kHdrWaveBytes;
+    static_assert(Lay::kHdr + Lay::kWaves * Lay::kCapStride <= (Lay::kL2 ? kA2Bytes : kLdsBytes), "captured header slots fit");
+    static_assert(4u * Lay::kCapBlocks * 256u <= Lay::kCapStride, "a wave's captured cells fit its stride");
+    const uint32_t hw = Lay::kHdr + wave * kHwStride;  // this wave's header slots
     // where the parse is parked until the finish: the header slot itself, or with chained tiles
     // (the next tile's header DMA lands before this tile's finish) the wave's scratch area,
     // which the one-pass kernel does not otherwise use
@@ -1241,7 +1335,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             const int rows = Tt.P - Tt.r0f;
             const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + (Tt.sdw() << 2));
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
+            for (int k = 0; k < Lay::kCapBlocks; ++k) {
                 if (Tt.len >= 4u && k < rows) {
                     const u32x4 v = load_row(fb, -(int)Tt.ph + 16 * k + 4 * (int)gl);
                     *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)(4 * k + (int)gl) * 256u + grp * 16u) = v;
@@ -1279,8 +1373,12 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         uint32_t len;
         if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(3);  // the preamble outranks other waves' row loops
         tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
-        if (FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
-        build_region_a(tabs, lds);
+        if constexpr (Lay::kL2) {
+            a2_tables_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
+        } else {
+            if (FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
+            build_region_a(tabs, lds);
+        }
         FS_STAMP(7);
         descriptors_ready<kOps>(S, len);
         FS_STAMP(8);
@@ -1293,13 +1391,13 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         }
         T.P = 0;
         if (first) {
-            tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
+            tile_geometry_a<kAl, Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
             FS_STAMP(11);
             if (!FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             FS_STAMP(12);
         }
     }
-    if (!FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);
+    if (!Lay::kL2 && !FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);
     bool x4 = false;
     auto first_rows = [&]() {
         if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
@@ -1363,7 +1461,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
                 else __builtin_amdgcn_s_waitcnt(0x0070);
             }
-            parse_tile<kOps, kSlotA>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
+            parse_tile<kOps, kSlotA, Lay::kL2>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
                        parser, pk, kCapture ? T.ph : 0u);
             if (FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             if (chain) tile_descriptors(tnext, grp, n, offsets, lengths, Sn, lenn, fpt);
@@ -1393,13 +1491,13 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 // consume the ring slot, then refill the SAME registers: no copy of an
                 // in-flight load, so the compiler keeps kPfA-1 loads outstanding
                 const bool masked = r < T.H;
-                if (kAl && masked) masked_row_al(lds, keys, pf[i], rel, T.nd(), T.sa(), T.tail_mask(), A, cs);
-                else if (masked) masked_row(lds, keys, pf[i], rel, load_pos(rel, T.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
-                else if (kAl && !kRefill && i == kPfA - 1) tail_row_al(lds, keys, pf[i], rel, T.nd(), T.tail_mask(), A, cs);
-                else lean_row(lds, keys, pf[i], A, cs);
-                if (kCapture && r0 == 0 && T.cap) {  // the frame's blocks 0..2 into the header slot
+                if (kAl && masked) masked_row_al<Lay::kRegion>(lds, keys, pf[i], rel, T.nd(), T.sa(), T.tail_mask(), A, cs);
+                else if (masked) masked_row<Lay::kRegion>(lds, keys, pf[i], rel, load_pos(rel, T.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
+                else if (kAl && !kRefill && i == kPfA - 1) tail_row_al<Lay::kRegion>(lds, keys, pf[i], rel, T.nd(), T.tail_mask(), A, cs);
+                else lean_row<Lay::kRegion>(lds, keys, pf[i], A, cs);
+                if (kCapture && r0 == 0 && T.cap) {  // the frame's first blocks into the header slot
                     const uint32_t k = (uint32_t)(i - T.r0f);
-                    if (k < 3u) *reinterpret_cast<u32x4*>(lds + hw + (4u * k + gl) * 256u + grp * 16u) = pf[i];
+                    if (k < (uint32_t)Lay::kCapBlocks) *reinterpret_cast<u32x4*>(lds + hw + (4u * k + gl) * 256u + grp * 16u) = pf[i];
                 }
                 if (kRefill) {
                     const int rn = rel + kRowDwords * kPfA;
@@ -1420,8 +1518,8 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
 #pragma unroll
             for (int i = 0; i < kPfA; ++i) {
                 if (kAl && !kRefill && i == kPfA - 1)
-                    tail_row_al(lds, keys, pf[i], T.rel0 + kRowDwords * (r0 + i), T.nd(), T.tail_mask(), A, cs);
-                else lean_row(lds, keys, pf[i], A, cs);
+                    tail_row_al<Lay::kRegion>(lds, keys, pf[i], T.rel0 + kRowDwords * (r0 + i), T.nd(), T.tail_mask(), A, cs);
+                else lean_row<Lay::kRegion>(lds, keys, pf[i], A, cs);
                 if (kRefill) {
                     pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
                 } else if (kKind == 2) {
@@ -1449,7 +1547,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                     // the next tile's descriptors are older than the ring's kPfA loads
                     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(Sn), "+v"(lenn) : "n"(kPfA));
                     if (kOps == kOpsFcs) lenn = lenn >= 4u ? lenn - 4u : 0u;
-                    tile_geometry_a<kAl>(Tn, tnext, grp, gl, n, Sn, lenn, frames, fpt);
+                    tile_geometry_a<kAl, Lay::kCapBlocks>(Tn, tnext, grp, gl, n, Sn, lenn, frames, fpt);
                     if (report && mode_b_worthy(Tn.nd()) && lane == 0u) post_report(report);
                     if (Rc < T.H) block(Rc, Next());
                     else lean_block(Rc, Next());
@@ -1490,9 +1588,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             for (uint32_t j = 0; j < 4; ++j) {
                 const uint32_t sh = (kq - j) & 15u, c = sh & 3u, a4 = sh >> 2;
                 uint32_t v = A[j];
-                const uint32_t v1 = zplain(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
+                const uint32_t v1 = Lay::z4c(lds, v, c);
                 v = c ? v1 : v;
-                const uint32_t v2 = zplain(lds, v, a4 == 1u ? kLdsZ16 : a4 == 2u ? kLdsZ32 : kLdsZ48);
+                const uint32_t v2 = Lay::z16a(lds, v, a4);
                 Y ^= a4 ? v2 : v;
             }
         } else {
@@ -1515,7 +1613,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         FS_STAMP(3);
         // ---- the group's lane 0: finish and store (its frame's parse comes back from LDS).
         if (parser)
-            finish_frame<kOps>(lds, P, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths,
+            finish_frame<kOps, Lay>(lds, P, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths,
                                tile * fpt + grp, out, status, tx);
         FS_STAMP(4);
         FS_RTSTAMP(6);
@@ -1527,7 +1625,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             uint32_t len;
             tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
             descriptors_ready<kOps>(S, len);
-            tile_geometry_a<kAl>(T, tile, grp, gl, n, S, len, frames, fpt);
+            tile_geometry_a<kAl, Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
             if (!FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             if (!kCapture) tile_header(T);
             if (T.P > 0) {
@@ -1824,6 +1922,10 @@ __device__ __forceinline__ uint32_t zshift_w(const char* lds, uint32_t v, uint32
 struct LayoutW {
     static constexpr uint32_t kZfin = kW_Zfin;
     __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift_w(lds, v, k); }
+    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
+        return zplain(lds, v, kZfin + 4096u * t);
+    }
+    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) { return lds32(lds, kZfin + 3u * 4096u + (i << 2)); }
 };
 
 // Region A in place: entry row e (256 B) = [op*32 + table*8 + copy], op 0 = Z_244, op 1 = Z_4.
@@ -2347,7 +2449,20 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH(K)                                                                                        \
     hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
-    const bool al = force == 0 || force == 4;  // the one-pass choice: block-aligned rows (force 1: end-anchored)
+    const bool al = force == 0 || force == 4 || force == 5;  // the one-pass choice: block-aligned rows (force 1: end-anchored)
+    // force 5: the block-aligned kernel as two 8-wave workgroups per CU (LayA2; RX ops only)
+    const bool dual = force == 5 && op != FsOp::kFill;
+    if (dual && !mixed) {
+        uint32_t b2 = (tiles + kA2Waves - 1) / kA2Waves;
+        if (b2 > 2u * max_blocks) b2 = 2u * max_blocks;
+#define FS_LAUNCH2(OPS)                                                                                         \
+    hipLaunchKernelGGL((digest_kernel_a<OPS, true, LayA2>), dim3(b2), dim3(kA2Waves * kWave), 0, stream, frames, offsets, \
+                       lengths, n, mtu, tables, o, status, report, wframes, tx, fpt)
+        if (op == FsOp::kDigest) FS_LAUNCH2(kOpsDigest);
+        else FS_LAUNCH2(kOpsFcs);
+#undef FS_LAUNCH2
+        return hipGetLastError();
+    }
     switch (op) {
     case FsOp::kDigest:
         if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));

@@ -43,6 +43,12 @@ void build_tables(FsTables* t) {
     for (uint32_t e = 0; e < 256; ++e)
         for (uint32_t b = 0; b < 4; ++b)
             for (uint32_t c = 0; c < 8; ++c) t->region_a[e][8 * b + c] = zrow[b][e];
+    for (int k = 0; k < 8; ++k) {  // the two-workgroups-per-CU kernel's plain tables
+        static uint32_t zk[4][256];
+        op_table(t1, kA2Tables[k], zk);
+        for (uint32_t e = 0; e < 256; ++e)
+            for (uint32_t b = 0; b < 4; ++b) t->region_a[e][32u + ((4u * k + b) ^ (e & 31u))] = zk[b][e];
+    }
     for (uint32_t b = 0; b < 4; ++b)
         for (uint32_t j = 0; j < 8; ++j) t->z64_basis[b][j] = zrow[b][1u << j];
     // region A entries are the XOR of the basis columns of their set bits (GF(2) linearity)

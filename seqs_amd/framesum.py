@@ -194,12 +194,14 @@ class Engine:
             raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
 
     # kernel variants (fs_ctx_set_kernel): results are identical, only the speed differs
-    KERNEL_AUTO, KERNEL_ONE_PASS, KERNEL_MIXED, KERNEL_WIDE, KERNEL_ALIGNED = 0, 1, 2, 3, 4
+    KERNEL_AUTO, KERNEL_ONE_PASS, KERNEL_MIXED, KERNEL_WIDE, KERNEL_ALIGNED, KERNEL_DUAL = 0, 1, 2, 3, 4, 5
 
     def set_kernel(self, variant: int) -> None:
-        """0: automatic (default: the 16-lane kernel); 1: the 4-lane one-pass kernel; 2: the
-        4-lane kernel that splits long frames of mixed-length tiles into pieces; 3: the 16-lane
-        kernel (256-byte rows, frames ordered by length into passes)."""
+        """0: automatic (the mixed-length kernel after a batch that had mixed-length tiles, the
+        block-aligned one-pass kernel otherwise); 1: the one-pass kernel with end-anchored rows;
+        2: the kernel that splits long frames of mixed-length tiles into pieces; 3: the 16-lane
+        kernel (256-byte rows, frames ordered by length into passes); 4: the one-pass kernel with
+        block-aligned rows; 5: the same as two 8-wave workgroups per CU (RX ops)."""
         self._check(self.lib.fs_ctx_set_kernel(self._ctx, int(variant)), "fs_ctx_set_kernel")
 
     # ---- device-resident path (torch tensors as device memory) -------------

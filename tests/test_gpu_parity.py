@@ -22,8 +22,8 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 @pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_WIDE, Engine.KERNEL_ALIGNED,
-                                        Engine.KERNEL_AUTO],
-                ids=["one_pass", "mixed", "wide", "aligned", "auto"])
+                                        Engine.KERNEL_DUAL, Engine.KERNEL_AUTO],
+                ids=["one_pass", "mixed", "wide", "aligned", "dual", "auto"])
 def engine(request):
     # every case through every kernel variant (and the automatic choice)
     if not torch.cuda.is_available():

@@ -15,6 +15,7 @@ from seqs_amd import Engine, synth  # noqa: E402
 p = argparse.ArgumentParser()
 p.add_argument("--config", default="c2")
 p.add_argument("--frames", type=int, default=65536)
+p.add_argument("--kernel", type=int, default=0)
 a = p.parse_args()
 dev = torch.device("cuda:0")
 bs = []
@@ -23,6 +24,7 @@ for b in range(4):
                     else synth.mixed_batch(a.frames, seed=2 + b))
     bs.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)))
 e = Engine(0)
+e.set_kernel(a.kernel)
 out = torch.empty((a.frames, 2), dtype=torch.int32, device=dev)
 st = torch.empty((a.frames,), dtype=torch.uint8, device=dev)
 for i in range(8):

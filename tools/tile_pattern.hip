@@ -30,8 +30,12 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 template <int G, int PF, int AL, int WPB>
 __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
-                                                    uint32_t* out) {
+                                                    uint32_t* out, uint32_t delay_10ns = 0) {
     constexpr int FPT = 64 / G;
+    if (delay_10ns) {  // `ovl`: a start phase of this length (the digest kernel's tables and geometry)
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < delay_10ns) __builtin_amdgcn_s_sleep(2);
+    }
     constexpr uint32_t RB = 16u * G;
     const uint32_t lane = threadIdx.x & 63u, grp = lane / G, gl = lane % G;
     const uint32_t gwave = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;  // wave-major
@@ -116,7 +120,7 @@ int main(int argc, char** argv) {
     hipDeviceProp_t prop;
     CHECK(hipGetDeviceProperties(&prop, 0));
     const int cus = prop.multiProcessorCount;
-    hipStream_t st[4];
+    hipStream_t st[5];
     for (auto& x : st) CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     printf("batch %u x %u B = %zu bytes, %d rotated, %d CUs\n", nf, flen, nbytes, NB, cus);
     const int reps = big ? 40 : calib ? 20 : 400;
@@ -146,6 +150,47 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((k_stream<PF, WPB>), dim3(cus * GRIDMUL), dim3(64 * WPB), 0, s,                \
                            (const u32x4*)bufs[i % NB], nbytes / 16, out);                                 \
     }, "stream PF=" #PF " waves/WG=" #WPB " WG/CU=" #GRIDMUL)
+    if (argc > 1 && std::string(argv[1]) == "ovl") {
+        // overlap of consecutive launches when a start phase precedes the rows: one 16-wave
+        // workgroup per CU (LDS-bound, as the digest kernel) against two 8-wave workgroups
+        auto ovl = [&](int wpb, size_t lds, uint32_t delay, const char* name) {
+            double res[2];
+            int k = 0;
+            for (int ns : {1, 5}) {
+                for (int pass = 0; pass < 2; ++pass) {
+                    CHECK(hipDeviceSynchronize());
+                    auto t0 = std::chrono::steady_clock::now();
+                    for (int i = 0; i < reps; ++i) {
+                        if (wpb == 16)
+                            hipLaunchKernelGGL((k_tiles<4, 5, 2, 16>), dim3(cus), dim3(1024), lds, st[i % ns],
+                                               bufs[i % NB], nf, flen, out, delay);
+                        else
+                            hipLaunchKernelGGL((k_tiles<4, 5, 2, 8>), dim3(cus * 2), dim3(512), lds, st[i % ns],
+                                               bufs[i % NB], nf, flen, out, delay);
+                    }
+                    CHECK(hipDeviceSynchronize());
+                    res[k] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+                }
+                ++k;
+            }
+            printf("%-44s 1 stream %9.2f us %7.0f GB/s | 5 streams %9.2f us %7.0f GB/s\n", name, res[0],
+                   nbytes / (res[0] * 1e-6) / 1e9, res[1], nbytes / (res[1] * 1e-6) / 1e9);
+        };
+        CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tiles<4, 5, 2, 16>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+        CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tiles<4, 5, 2, 8>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
+        for (int rep = 0; rep < 2; ++rep) {
+            for (uint32_t d : {0u, 300u, 500u}) {
+                char nm[96];
+                snprintf(nm, sizeof nm, "16 waves, 150 KB, 1 WG/CU, start %u ns", d * 10);
+                ovl(16, 150 * 1024, d, nm);
+                snprintf(nm, sizeof nm, "8 waves, 80 KB, 2 WG/CU, start %u ns", d * 10);
+                ovl(8, 80 * 1024, d, nm);
+            }
+        }
+        return 0;
+    }
     if (calib) {  // FETCH_SIZE calibration under rocprofv3 (98,304,000 B per launch)
         STREAM(4, 16, 1);
         TILES(4, 5, 2, 16);
