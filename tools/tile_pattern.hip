@@ -54,7 +54,9 @@ __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ 
         if (AL) {
             const uint64_t b0 = S / RB, b1 = (E - 1) / RB;
             if (b0 + (uint64_t)r > b1) return false;
-            a = (b0 + r) * RB + 16u * gl;
+            // AL 3: whole blocks, the odd groups' frames read backwards (last block first), so the
+            // 128-B line a frame shares with the next one is read by both at the same time
+            a = ((AL == 3 && (grp & 1u)) ? b1 - r : b0 + r) * RB + 16u * gl;
             if (AL == 1 && (a + 16 <= S || a >= E)) return false;  // AL 2: whole blocks, as the kernel loads
         } else {
             const uint64_t E4 = (E + 3) & ~uint64_t(3);
@@ -104,9 +106,11 @@ __global__ void __launch_bounds__(64 * WPB) k_stream(const u32x4* __restrict__ p
 }
 
 int main(int argc, char** argv) {
-    const uint32_t flen = 1500;
+    // `dir [flen]`: forward-only (AL 2) against alternating-direction (AL 3) whole blocks
+    const bool dir = argc > 1 && std::string(argv[1]).rfind("dir", 0) == 0;
+    const uint32_t flen = dir && argc > 2 ? (uint32_t)atoi(argv[2]) : 1500;
     const bool big = argc > 1 && std::string(argv[1]) == "c4";
-    const uint32_t nf = big ? (1u << 20) : 65536u;
+    const uint32_t nf = big ? (1u << 20) : (uint32_t)(98304000ull / flen);
     const size_t nbytes = (size_t)nf * flen;
     const bool calib = argc > 1 && std::string(argv[1]) == "calib";
     const int NB = big ? 2 : 6;
@@ -123,7 +127,8 @@ int main(int argc, char** argv) {
     hipStream_t st[5];
     for (auto& x : st) CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     printf("batch %u x %u B = %zu bytes, %d rotated, %d CUs\n", nf, flen, nbytes, NB, cus);
-    const int reps = big ? 40 : calib ? 20 : 400;
+    const bool dircal = argc > 1 && std::string(argv[1]) == "dircal";
+    const int reps = big ? 40 : (calib || dircal) ? 20 : 400;
     auto run = [&](auto launch, const char* name) {
         double res[2];
         int k = 0;
@@ -189,6 +194,14 @@ int main(int argc, char** argv) {
                 ovl(8, 80 * 1024, d, nm);
             }
         }
+        return 0;
+    }
+    if (dir) {
+        STREAM(4, 16, 1);
+        TILES(4, 5, 2, 16);
+        TILES(4, 5, 3, 16);
+        TILES(4, 5, 2, 16);
+        TILES(4, 5, 3, 16);
         return 0;
     }
     if (calib) {  // FETCH_SIZE calibration under rocprofv3 (98,304,000 B per launch)
