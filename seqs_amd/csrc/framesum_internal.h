@@ -31,11 +31,18 @@ struct FsTables {
     uint32_t z768[4][256];     // Z_768: one full piece (mode B Horner over a frame's pieces)
     // --- not part of the LDS image ---
     uint32_t z64_basis[4][8];  // Z_64[b][1 << j]: region A's entries are XORs of these
+    // T[b][1 << j] of the 40 plain [4][256] tables above, in LDS-image order (piece p = 4 t + b is the
+    // 1-KB piece at LDS byte 1024 p): the kernels build them in place by VALU, as region A
+    uint32_t plain_basis[40][8];
+    // T_(kA2Tables[q >> 2])[q & 3][1 << j]: the bases of region A's upper-half plain tables (LayA2)
+    uint32_t a2_basis[32][8];
 };
 constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 10;  // the LDS image: everything before z64_basis
 // region A's plain tables (slots 32..63): the zero shift in bytes of table t = 0..7
 constexpr int kA2Tables[8] = {4, 8, 12, 16, 32, 48, 2, 1};
 static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout");
+static_assert(offsetof(FsTables, z32) == 65536 && offsetof(FsTables, plain_basis) == kTablesLdsBytes + 128,
+              "FsTables layout: the plain tables are 40 1-KB pieces after region A");
 
 void build_tables(FsTables* t);
 

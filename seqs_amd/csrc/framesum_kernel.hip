@@ -95,6 +95,12 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FS_CHAIN 0  // block-aligned one-pass kernel: chained tiles (the ring runs on across a wave's
                     // tiles); parity-green, C4 within noise of the unchained kernel
 #endif
+#ifndef FS_PLAIN_VALU
+#define FS_PLAIN_VALU 1  // the plain tables built in place by VALU from their bases (0: copied by LDS-DMA)
+#endif
+#ifndef FS_A2_VALU
+#define FS_A2_VALU 1  // two-workgroups-per-CU kernel: region A built in place by VALU (0: copied by LDS-DMA)
+#endif
 #ifndef FS_PRIO_MIN
 #define FS_PRIO_MIN 36  // ... for tiles of more rows than this
 #endif
@@ -1062,20 +1068,40 @@ __device__ __forceinline__ void prefetch_unit(const Unit& U, u32x4 (&pf)[kPrefet
     }
 }
 
-// Region A in place: thread t builds Z64[b][e] (b = t >> 8, e = t & 255) as the XOR of
-// the basis columns of e's set bits and stores its 8 copies (32 contiguous bytes).
-// The basis row comes in by a scalar load (lgkmcnt), so waiting for it never waits for the
-// descriptors' vector loads issued before it.
+// The tables in place. Region A: thread t builds Z64[b][e] (b = t >> 8, e = t & 255) as the XOR
+// of the basis columns of e's set bits and stores its 8 copies (32 contiguous bytes). The plain
+// tables (FS_PLAIN_VALU): wave w builds the 1-KB pieces p = w, w + 16, w + 32 (< 40) of the
+// 40 [4][256] tables the same way, lane l the entries 4l .. 4l + 3 (one ds_write_b128): no
+// LDS-DMA in the preamble's vector-memory burst, no wait for table pieces at the barrier.
+// The bases come in by scalar loads (lgkmcnt), all issued before one wait, so waiting for them
+// never waits for the descriptors' vector loads issued before them.
+__device__ __forceinline__ uint64_t sgpr_addr(const void* p) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+}
 __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs, char* lds) {
     typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
     const uint32_t t = threadIdx.x;
     const uint32_t b = __builtin_amdgcn_readfirstlane(t >> 8);  // wave-uniform (64 | 256)
     const uint32_t e = t & 255u;
-    const uint64_t a = reinterpret_cast<uint64_t>(&tabs->z64_basis[b][0]);
-    const uint64_t sa = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint64_t sa = sgpr_addr(&tabs->z64_basis[b][0]);
     u32x8 basis;
+#if FS_PLAIN_VALU
+    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint32_t lane = t & 63u;
+    const uint64_t s0 = sgpr_addr(&tabs->plain_basis[w][0]);
+    const uint64_t s1 = sgpr_addr(&tabs->plain_basis[w + 16u][0]);
+    const uint64_t s2 = sgpr_addr(&tabs->plain_basis[min(w + 32u, 39u)][0]);
+    u32x8 pb0, pb1, pb2;
+    asm volatile(
+        "s_load_dwordx8 %0, %4, 0x0\n\ts_load_dwordx8 %1, %5, 0x0\n\t"
+        "s_load_dwordx8 %2, %6, 0x0\n\ts_load_dwordx8 %3, %7, 0x0\n\ts_waitcnt lgkmcnt(0)"
+        : "=&s"(basis), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
+        : "s"(sa), "s"(s0), "s"(s1), "s"(s2));
+#else
     asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(basis) : "s"(sa));
+#endif
     uint32_t v = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
@@ -1085,6 +1111,18 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
     u32x4* dst = reinterpret_cast<u32x4*>(lds + kLdsRegionA + e * 256u + 32u * b);
     dst[0] = u32x4{v, v, v, v};
     dst[1] = u32x4{v, v, v, v};
+#if FS_PLAIN_VALU
+    auto piece = [&](const u32x8& pb, uint32_t p) {
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
+        const uint32_t x1 = x ^ pb[0];
+        *reinterpret_cast<u32x4*>(lds + 1024u * p + 16u * lane) = u32x4{x, x1, x ^ pb[1], x1 ^ pb[1]};
+    };
+    piece(pb0, w);
+    piece(pb1, w + 16u);
+    if (w + 32u < 40u) piece(pb2, w + 32u);
+#endif
 }
 // LDS-DMA by inline asm: invisible to hipcc's vmcnt model (the builtin makes it drain later
 // LDS reads with vmcnt(0)); unknown VMEM ops only make the compiler's own counted waits
@@ -1118,7 +1156,7 @@ __device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, con
     const uint32_t lds0 = lds_base(lds);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
-    for (uint32_t k = 0; k < ((FS_DIAG & 2) ? 0 : kDmaPerWave); ++k) {
+    for (uint32_t k = 0; k < (((FS_DIAG & 2) || FS_PLAIN_VALU) ? 0 : kDmaPerWave); ++k) {
         const uint32_t c = min(w0 + k * kWavesPerBlock, kPlainChunks - 1u);
         dma_x4(reinterpret_cast<const char*>(tabs) + (kPlainChunk0 + c) * 1024u + lane * 16u,
                __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
@@ -1250,6 +1288,57 @@ struct LayA2 {
     }
 };
 
+// LayA2's tables built in place by VALU (FS_A2_VALU), in FsTables::region_a's layout: thread t
+// builds Z64[b][e] for e = t & 255 and b = 2 (t >> 8), 2 (t >> 8) + 1 (8 copies each); wave w builds
+// the upper-half plain pieces q = w + 8k (k = 0..3), lane l the entries 4l .. 4l + 3 of each. All
+// six bases by scalar loads issued before one wait (no vector-memory op at all).
+__device__ __forceinline__ void a2_tables_build(const FsTables* __restrict__ tabs, char* lds, uint32_t wave,
+                                                uint32_t lane) {
+    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    const uint32_t t = threadIdx.x;
+    const uint32_t h = __builtin_amdgcn_readfirstlane(t >> 8);
+    const uint32_t e = t & 255u;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(wave);
+    const uint64_t a0 = sgpr_addr(&tabs->z64_basis[2u * h][0]), a1 = sgpr_addr(&tabs->z64_basis[2u * h + 1u][0]);
+    const uint64_t q0 = sgpr_addr(&tabs->a2_basis[w][0]), q1 = sgpr_addr(&tabs->a2_basis[w + 8u][0]);
+    const uint64_t q2 = sgpr_addr(&tabs->a2_basis[w + 16u][0]), q3 = sgpr_addr(&tabs->a2_basis[w + 24u][0]);
+    u32x8 z0, z1, p0, p1, p2, p3;
+    asm volatile(
+        "s_load_dwordx8 %0, %6, 0x0\n\ts_load_dwordx8 %1, %7, 0x0\n\ts_load_dwordx8 %2, %8, 0x0\n\t"
+        "s_load_dwordx8 %3, %9, 0x0\n\ts_load_dwordx8 %4, %10, 0x0\n\ts_load_dwordx8 %5, %11, 0x0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(z0), "=&s"(z1), "=&s"(p0), "=&s"(p1), "=&s"(p2), "=&s"(p3)
+        : "s"(a0), "s"(a1), "s"(q0), "s"(q1), "s"(q2), "s"(q3));
+    uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t m = 0u - ((e >> j) & 1u);
+        v0 ^= z0[j] & m;
+        v1 ^= z1[j] & m;
+    }
+    u32x4* dst = reinterpret_cast<u32x4*>(lds + e * 256u + 64u * h);
+    dst[0] = u32x4{v0, v0, v0, v0};
+    dst[1] = u32x4{v0, v0, v0, v0};
+    dst[2] = u32x4{v1, v1, v1, v1};
+    dst[3] = u32x4{v1, v1, v1, v1};
+    auto piece = [&](const u32x8& pb, uint32_t q) {
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
+        const uint32_t x1 = x ^ pb[0];
+        const uint32_t xv[4] = {x, x1, x ^ pb[1], x1 ^ pb[1]};
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t en = 4u * lane + i;
+            *reinterpret_cast<uint32_t*>(lds + (en << 8) + 128u + ((q ^ (en & 31u)) << 2)) = xv[i];
+        }
+    };
+    piece(p0, w);
+    piece(p1, w + 8u);
+    piece(p2, w + 16u);
+    piece(p3, w + 24u);
+}
+
 // LayA2's tables: region A's 64 KB as FsTables holds it (Z64's copies and the plain tables), 8
 // pieces of 1 KB per wave. (Building the Z64 half in place and copying only the plain tables'
 // 32 KB, lane-masked, measured 2-3% slower: the basis loads wait behind the DMAs.)
@@ -1374,7 +1463,8 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(3);  // the preamble outranks other waves' row loops
         tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
         if constexpr (Lay::kL2) {
-            a2_tables_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
+            if (FS_A2_VALU) a2_tables_build(tabs, lds, wave, lane);
+            else a2_tables_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
         } else {
             if (FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
             build_region_a(tabs, lds);

@@ -48,6 +48,8 @@ void build_tables(FsTables* t) {
         op_table(t1, kA2Tables[k], zk);
         for (uint32_t e = 0; e < 256; ++e)
             for (uint32_t b = 0; b < 4; ++b) t->region_a[e][32u + ((4u * k + b) ^ (e & 31u))] = zk[b][e];
+        for (uint32_t b = 0; b < 4; ++b)
+            for (uint32_t j = 0; j < 8; ++j) t->a2_basis[4 * k + b][j] = zk[b][1u << j];
     }
     for (uint32_t b = 0; b < 4; ++b)
         for (uint32_t j = 0; j < 8; ++j) t->z64_basis[b][j] = zrow[b][1u << j];
@@ -66,6 +68,17 @@ void build_tables(FsTables* t) {
     op_table(t1, 12, t->z12);
     op_table(t1, 8, t->z8);
     op_table(t1, 768, t->z768);
+    // the plain tables' bases (every [4][256] table is GF(2)-linear in its byte, as region A)
+    const uint32_t* plain = &t->z32[0][0];
+    for (uint32_t p = 0; p < 40; ++p)
+        for (uint32_t j = 0; j < 8; ++j) t->plain_basis[p][j] = plain[256 * p + (1u << j)];
+    for (uint32_t p = 0; p < 40; ++p)
+        for (uint32_t e = 0; e < 256; ++e) {
+            uint32_t v = 0;
+            for (uint32_t j = 0; j < 8; ++j)
+                if ((e >> j) & 1u) v ^= t->plain_basis[p][j];
+            if (v != plain[256 * p + e]) throw std::logic_error("plain table basis mismatch");
+        }
     // The final step Z_(4-t) replaces "Z_4 then undo t appended zero bytes"; Z_1[0] is the
     // standard byte table used for frames shorter than 4 bytes.
     if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");
