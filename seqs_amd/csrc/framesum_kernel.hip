@@ -61,7 +61,8 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FS_TXDIAG 0  // diagnostic builds only: 1 skips the fill's CRC correction, 2 its field stores, 4 the FCS stores
 #endif
 #ifndef FS_DIAG
-#define FS_DIAG 0  // diagnostic builds only (wrong results): 1 no header DMA, 2 no plain-table DMA
+#define FS_DIAG 0  // diagnostic builds only (wrong results): 1 no header DMA, 2 no plain-table DMA, 16 no parse,
+                   // 32 no finish (one-pass kernel)
 #endif
 #ifndef FS_AGE_PRIO
 #define FS_AGE_PRIO 1  // one-pass kernel: a SIMD's later-started waves get the higher issue priority
@@ -1551,8 +1552,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
                 else __builtin_amdgcn_s_waitcnt(0x0070);
             }
-            parse_tile<kOps, kSlotA, Lay::kL2>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
-                       parser, pk, kCapture ? T.ph : 0u);
+            if (!(FS_DIAG & 16))  // (diagnostic builds: 16 skips the parse)
+                parse_tile<kOps, kSlotA, Lay::kL2>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
+                           parser, pk, kCapture ? T.ph : 0u);
             if (FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             if (chain) tile_descriptors(tnext, grp, n, offsets, lengths, Sn, lenn, fpt);
         };
@@ -1702,7 +1704,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         cs += dpp_quad<kQuadXor2>(cs);
         FS_STAMP(3);
         // ---- the group's lane 0: finish and store (its frame's parse comes back from LDS).
-        if (parser)
+        if ((FS_DIAG & 32) && parser)  // (diagnostic builds: 32 stores the raw combine, no finish)
+            out[tile * fpt + grp] = uint2{Y, cs};
+        else if (parser)
             finish_frame<kOps, Lay>(lds, P, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths,
                                tile * fpt + grp, out, status, tx);
         FS_STAMP(4);
