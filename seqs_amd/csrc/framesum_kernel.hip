@@ -96,6 +96,10 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FS_CHAIN 0  // block-aligned one-pass kernel: chained tiles (the ring runs on across a wave's
                     // tiles); parity-green, C4 within noise of the unchained kernel
 #endif
+#ifndef FS_REPORT_AFTER_ROWS
+#define FS_REPORT_AFTER_ROWS 1  // block-aligned one-pass kernel: the first tile's mixed-length report check after
+                                // its first rows are issued (0: before them)
+#endif
 #ifndef FS_PLAIN_VALU
 #define FS_PLAIN_VALU 1  // the plain tables built in place by VALU from their bases (0: copied by LDS-DMA)
 #endif
@@ -1484,7 +1488,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         if (first) {
             tile_geometry_a<kAl, Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
             FS_STAMP(11);
-            if (!FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+            // (block-aligned rows with header capture: the report after the first rows' issue, below)
+            if (!FS_LATE_REPORT && !(kCapture && FS_REPORT_AFTER_ROWS) && report && mode_b_worthy(T.nd()) && lane == 0u)
+                post_report(report);
             FS_STAMP(12);
         }
     }
@@ -1502,6 +1508,8 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     // (FS_ROWS_FIRST: the first rows before the header DMA -- still older than the first
     // block's refills, which is all the parse's vmcnt(kPfA) needs; measured within noise)
     if (FS_ROWS_FIRST || kCapture) first_rows();
+    if (kCapture && FS_REPORT_AFTER_ROWS && !FS_LATE_REPORT && first && report && mode_b_worthy(T.nd()) && lane == 0u)
+        post_report(report);
     if (first) x4 = tile_header(T);
     FS_STAMP(13);
     if (!FS_ROWS_FIRST && !kCapture) first_rows();
