@@ -100,6 +100,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FS_REPORT_AFTER_ROWS 1  // block-aligned one-pass kernel: the first tile's mixed-length report check after
                                 // its first rows are issued (0: before them)
 #endif
+#ifndef FS_EARLY_ROWS
+#define FS_EARLY_ROWS 1  // block-aligned one-pass kernel: the first tile's H and capture flag after its first rows' issue
+#endif
 #ifndef FS_PLAIN_VALU
 #define FS_PLAIN_VALU 1  // the plain tables built in place by VALU from their bases (0: copied by LDS-DMA)
 #endif
@@ -1006,7 +1009,21 @@ struct TileA {
 // it, the last one ending on the block boundary after the frame end (nd + ealign() dwords from
 // frame dword 0), so a row load never straddles a line; the end-anchored rows otherwise
 // (ending at the frame's dword-rounded end).
+// The tile's masked-row count H and its capture flag (the last part of tile_geometry_a; the first
+// tile of the block-aligned kernel computes them after its first rows are issued, kDeferTail).
 template <bool kAl, int kCapBlocks = 3>
+__device__ __forceinline__ void tile_geometry_a_tail(TileA& T) {
+    const int nd = T.nd();
+    const int ndb = (kAl && nd > 0) ? nd + T.ealign() : nd;
+    T.cap = __ballot(nd > 0 && min(T.r0f + kCapBlocks, T.P) > kRingA<kAl>) == 0;
+    // Masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
+    // dword before the frame. The group's lane 0 has the lowest rel: row r is lean for the
+    // group once nd - 16 P + 16 r >= 2.
+    const int need = 2 - (ndb - kRowDwords * T.P);
+    const int h = (nd > 0 && need > 0) ? (need + kRowDwords - 1) / kRowDwords : 0;
+    T.H = min(group_max(h), T.P);
+}
+template <bool kAl, int kCapBlocks = 3, bool kDeferTail = false>
 __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
                                               uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
                                               uint32_t fpt) {
@@ -1019,7 +1036,6 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     const int R = group_max(rows);
     T.P = (R + kRingA<kAl> - 1) / kRingA<kAl> * kRingA<kAl>;
     T.r0f = nd > 0 ? T.P - rows : (1 << 20);
-    T.cap = __ballot(nd > 0 && min(T.r0f + kCapBlocks, T.P) > kRingA<kAl>) == 0;
     uint64_t ld_sdw = T.sdw();
     int ld_nd = ndb;
     uint32_t ld_ph = T.ph;
@@ -1046,12 +1062,7 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     // below it reloads the lane's chunk of that block (a row inside a block that holds a frame
     // byte never leaves that byte's page, so it needs no other clamp).
     T.lo = kAl ? -(int)ld_ph : max(ld_sdw > (1u << 24) ? -(1 << 24) : -(int)ld_sdw, min(0, ld_nd - 4));
-    // Masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
-    // dword before the frame. The group's lane 0 has the lowest rel: row r is lean for the
-    // group once nd - 16 P + 16 r >= 2.
-    const int need = 2 - (ndb - kRowDwords * T.P);
-    const int h = (nd > 0 && need > 0) ? (need + kRowDwords - 1) / kRowDwords : 0;
-    T.H = min(group_max(h), T.P);
+    if (!kDeferTail) tile_geometry_a_tail<kAl, kCapBlocks>(T);
 }
 
 // Frame dword at which a masked row's chunk is loaded: where it lies, unless it starts
@@ -1409,6 +1420,8 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     // No header DMA: its 2 KB per wave were 0.5 us of the preamble's vector-memory burst. 3 KB
     // per wave (12 cells), overlapping the wave scratch the one-pass kernel leaves unused.
     constexpr bool kCapture = kAl && FS_HDR_CAPTURE;
+    // the first tile's masked-row count and capture flag after its first rows are issued
+    constexpr bool kEarlyRows = kCapture && FS_EARLY_ROWS;
     constexpr uint32_t kHwStride = kCapture ? Lay::kCapStride : kHdrWaveBytes;
     static_assert(Lay::kHdr + Lay::kWaves * Lay::kCapStride <= (Lay::kL2 ? kA2Bytes : kLdsBytes), "captured header slots fit");
     static_assert(4u * Lay::kCapBlocks * 256u <= Lay::kCapStride, "a wave's captured cells fit its stride");
@@ -1486,7 +1499,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         }
         T.P = 0;
         if (first) {
-            tile_geometry_a<kAl, Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
+            tile_geometry_a<kAl, Lay::kCapBlocks, kEarlyRows>(T, tile, grp, gl, n, S, len, frames, fpt);
             FS_STAMP(11);
             // (block-aligned rows with header capture: the report after the first rows' issue, below)
             if (!FS_LATE_REPORT && !(kCapture && FS_REPORT_AFTER_ROWS) && report && mode_b_worthy(T.nd()) && lane == 0u)
@@ -1501,13 +1514,15 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
 #pragma unroll
             for (int i = 0; i < kPfA; ++i) {
                 const int rel = T.rel0 + kRowDwords * i;
-                pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
+                // (block-aligned rows: lpos is the identity on lean rows, so H is not needed here)
+                pf[i] = load_row(T.gfb, (kEarlyRows || i < T.H) ? lpos(rel, T.lo) : rel);
             }
         }
     };
     // (FS_ROWS_FIRST: the first rows before the header DMA -- still older than the first
     // block's refills, which is all the parse's vmcnt(kPfA) needs; measured within noise)
     if (FS_ROWS_FIRST || kCapture) first_rows();
+    if (kEarlyRows && first) tile_geometry_a_tail<kAl, Lay::kCapBlocks>(T);
     if (kCapture && FS_REPORT_AFTER_ROWS && !FS_LATE_REPORT && first && report && mode_b_worthy(T.nd()) && lane == 0u)
         post_report(report);
     if (first) x4 = tile_header(T);
