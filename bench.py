@@ -411,6 +411,11 @@ def main():
                                        "consecutive launches overlap each other's start and tail)",
                 "traffic": traffic,
                 "traffic_calibrated": traffic_cal,
+                "traffic_note": "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch (profiles/pmc_<cfg>.json, separate "
+                                "--pmc passes). Its excess over the algorithmic bytes is mostly the read pattern's own: "
+                                "the line two neighbouring frames share is fetched twice (~8.4% on C2); "
+                                "traffic_calibrated divides that pattern factor out (the kernel's excess beyond it)"
+                if traffic is not None else None,
                 "kernel": "digest_kernel",
                 "kernel_avg_us": round(k_avg_ms * 1e3, 3),
                 "kernel_timing": "HIP events around K back-to-back launches on the launch stream",

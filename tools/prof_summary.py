@@ -103,7 +103,11 @@ def main():
             f = c["pattern_factor"][c["config_pattern"][cfg]]
             out["hbm_bytes_per_launch_calibrated"] = int(round(out["hbm_bytes_per_launch"] / f))
             out["calibration_note"] = (f"divided by {f}: the doubled FETCH_SIZE of this access pattern without "
-                                       "compute over its true bytes (profiles/fetch_size_calibration.json)")
+                                       "compute over its true bytes (profiles/fetch_size_calibration.json). That "
+                                       "factor is real traffic of the pattern, not a counter artefact: the 128-B line "
+                                       "two neighbouring frames share is fetched twice (reading alternate frames "
+                                       "backwards fetches it once: profiles/round2/tile_pattern_dir_fetch.txt), so "
+                                       "this figure is the kernel's traffic beyond its read pattern's own")
         if "TCC_HIT_sum" in med and "TCC_MISS_sum" in med:
             out["l2_hit_rate"] = med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"])
         with open(os.path.join(dst, f"pmc_{cfg}.json"), "w") as f:
