@@ -103,6 +103,10 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_EARLY_ROWS
 #define FS_EARLY_ROWS 1  // block-aligned one-pass kernel: the first tile's H and capture flag after its first rows' issue
 #endif
+#ifndef FS_TABLES_BARRIER
+#define FS_TABLES_BARRIER 0  // one-pass kernel: 1 = the tables barrier right after the in-place build, before the descriptors'
+                             // wait (measured 1.3 us slower on C2: the waves then issue their first rows in one burst)
+#endif
 #ifndef FS_PLAIN_VALU
 #define FS_PLAIN_VALU 1  // the plain tables built in place by VALU from their bases (0: copied by LDS-DMA)
 #endif
@@ -1422,6 +1426,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     constexpr bool kCapture = kAl && FS_HDR_CAPTURE;
     // the first tile's masked-row count and capture flag after its first rows are issued
     constexpr bool kEarlyRows = kCapture && FS_EARLY_ROWS;
+    // the tables barrier right after the in-place table build (FS_TABLES_BARRIER; only when no table
+    // comes by LDS-DMA): each wave then issues and consumes its first rows on its own descriptors
+    constexpr bool kTablesBarrier =
+        FS_TABLES_BARRIER && !FS_EARLY_BARRIER && FS_PLAIN_VALU && (!Lay::kL2 || FS_A2_VALU) && !(FS_DIAG & 2);
     constexpr uint32_t kHwStride = kCapture ? Lay::kCapStride : kHdrWaveBytes;
     static_assert(Lay::kHdr + Lay::kWaves * Lay::kCapStride <= (Lay::kL2 ? kA2Bytes : kLdsBytes), "captured header slots fit");
     static_assert(4u * Lay::kCapBlocks * 256u <= Lay::kCapStride, "a wave's captured cells fit its stride");
@@ -1487,6 +1495,12 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             if (FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
             build_region_a(tabs, lds);
         }
+        if (kTablesBarrier) {
+            // every table is built in place (no DMA): one barrier on this wave's LDS stores, while its
+            // descriptors are still in flight -- after it no wave waits for another's descriptors
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
+            __builtin_amdgcn_s_barrier();
+        }
         FS_STAMP(7);
         descriptors_ready<kOps>(S, len);
         FS_STAMP(8);
@@ -1529,7 +1543,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     FS_STAMP(13);
     if (!FS_ROWS_FIRST && !kCapture) first_rows();
     FS_STAMP(9);
-    if (FS_EARLY_BARRIER) {
+    if (FS_EARLY_BARRIER || kTablesBarrier) {
         // (the tables were ready at the early barrier)
     } else if (kCapture) {  // no header DMA: the table pieces are older than the rows
         if (first && T.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
@@ -1538,7 +1552,8 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         tables_landed<kPfA, kSlotA>(first, T.P > 0, x4);
     }
     FS_STAMP(10);
-    if (!FS_EARLY_BARRIER) __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    if (!FS_EARLY_BARRIER && !kTablesBarrier)
+        __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(0);
     if (FS_AGE_PRIO) {  // the SIMD's younger waves (wave >> 2: its 4 waves in launch order) outrank the older
         const uint32_t w = __builtin_amdgcn_readfirstlane(wave) >> 2;
