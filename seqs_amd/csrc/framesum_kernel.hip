@@ -107,6 +107,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #define FS_TABLES_BARRIER 0  // one-pass kernel: 1 = the tables barrier right after the in-place build, before the descriptors'
                              // wait (measured 1.3 us slower on C2: the waves then issue their first rows in one burst)
 #endif
+#ifndef FS_AB_ROWS_FIRST
+#define FS_AB_ROWS_FIRST 1  // mixed-length kernel: the first tile's rows before its header DMA
+#endif
 #ifndef FS_PLAIN_VALU
 #define FS_PLAIN_VALU 1  // the plain tables built in place by VALU from their bases (0: copied by LDS-DMA)
 #endif
@@ -1832,8 +1835,11 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     }
     if (!FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);
     bool x4 = false;
+    // FS_AB_ROWS_FIRST: the first rows ahead of the header DMA (still older than the first block's
+    // refills, which is all the parse's vmcnt(kPrefetch) needs)
+    if (FS_AB_ROWS_FIRST && first) prefetch_unit(U, pf);
     if (first) x4 = header_dma<false>(T, frames, lds, hw, gl0, lane);
-    if (first) prefetch_unit(U, pf);
+    if (!FS_AB_ROWS_FIRST && first) prefetch_unit(U, pf);
     FS_STAMP(9);
     tables_landed<kPrefetch>(first, U.P > 0, x4);
     FS_STAMP(10);
