@@ -227,6 +227,12 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
  * are identical in every case; only the speed differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
+/* The variant (1..5, as above) the context's latest launch ran; 0 before its first
+ * launch, FS_E_INVALID for a null context. With variant 0 a context's first 16
+ * launches run the mixed-length kernel (2), which keeps itself chosen while it
+ * meets mixed tiles; uniform traffic then moves to the one-pass kernel (4). */
+int fs_ctx_last_kernel(const fs_ctx* ctx);
+
 /* Pinned host memory helpers for fs_digest_batch_host callers. */
 fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out);
 fs_status fs_host_free(fs_ctx* ctx, void* p);

@@ -172,7 +172,9 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
         e = hipHostMalloc(&hp, 64, hipHostMallocMapped);
         if (e == hipSuccess) {
             ctx->h_report = static_cast<volatile uint32_t*>(hp);
-            *ctx->h_report = 0u;
+            ctx->h_report[framesum::kReportLatest] = 0u;
+            ctx->h_report[framesum::kReportInitial] = framesum::kInitialMixedLaunches;
+            ctx->h_report[framesum::kReportChosen] = 0u;
             e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_report), hp, 0);
         }
     }
@@ -493,6 +495,11 @@ fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (variant < 0 || variant > 5) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0..5");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
+}
+
+int fs_ctx_last_kernel(const fs_ctx* ctx) {
+    if (!ctx || !ctx->h_report) return FS_E_INVALID;
+    return (int)ctx->h_report[framesum::kReportChosen];
 }
 
 fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out) {

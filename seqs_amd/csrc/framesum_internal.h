@@ -86,6 +86,11 @@ enum class FsOp { kDigest, kFill, kFcs };
 // force 1 keeps the end-anchored rows).
 // `tables_w`: the 16-lane kernel's tables; force 3 = the 16-lane kernel (an experimental variant,
 // parity-tested like the others; slower than the 4-lane kernels on the benchmark configs).
+// The context's host-mapped report block (64 B): word kReportLatest is written by the device (the
+// latest launch id that met mixed-length tiles); the others only by the host: the launches left in
+// the context's initial mixed-kernel window, and the variant of its latest launch.
+constexpr int kReportLatest = 0, kReportInitial = 1, kReportChosen = 2;
+constexpr uint32_t kInitialMixedLaunches = 16;
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
                          int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force = 0,

@@ -2558,10 +2558,23 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     const uint64_t report = can_report ? rdev | ((uint64_t)id << 48) : 0u;
     bool mixed = false;
     if (can_report) {
-        const uint32_t latest = *report_host;
+        const uint32_t latest = report_host[kReportLatest];
         mixed = latest != 0u && ((id - latest) & 0xFFFFu) <= kStickyLaunches;
+        // A context's first launches run the mixed-length kernel: it reports its own mode-B tiles,
+        // so mixed traffic keeps it from the first batch on (the one-pass kernel's report would
+        // arrive launches late, after slow first batches), and uniform traffic moves to the
+        // one-pass kernel once the window ends (host-only word: the device never writes it).
+        const uint32_t left = report_host[kReportInitial];
+        if (left != 0u) {
+            report_host[kReportInitial] = left - 1u;
+            mixed = true;
+        }
     }
     if (force) mixed = force == 2;
+    // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
+    auto chosen = [&](uint32_t v) {
+        if (report_host) report_host[kReportChosen] = v;
+    };
     // Fewer frames per tile (8, then 4) while 16 would leave waves without a tile: a small
     // batch still spreads over every CU. The groups past a tile's frames stay empty in the
     // one-pass kernel; the mixed-length kernel gives them pieces of the tile's long frames.
@@ -2576,6 +2589,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH_W(OPS)                                                                                       \
     hipLaunchKernelGGL((digest_kernel_w<OPS>), dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, \
                        mtu, tables_w, o, status, wframes, tx, fpt)
+        chosen(3u);
         switch (op) {
         case FsOp::kDigest: FS_LAUNCH_W(kOpsDigest); break;
         case FsOp::kFill: FS_LAUNCH_W(kOpsTx); break;
@@ -2596,11 +2610,13 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH2(OPS)                                                                                         \
     hipLaunchKernelGGL((digest_kernel_a<OPS, true, LayA2>), dim3(b2), dim3(kA2Waves * kWave), 0, stream, frames, offsets, \
                        lengths, n, mtu, tables, o, status, report, wframes, tx, fpt)
+        chosen(5u);
         if (op == FsOp::kDigest) FS_LAUNCH2(kOpsDigest);
         else FS_LAUNCH2(kOpsFcs);
 #undef FS_LAUNCH2
         return hipGetLastError();
     }
+    chosen(mixed ? 2u : al ? 4u : 1u);
     switch (op) {
     case FsOp::kDigest:
         if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));

@@ -67,6 +67,7 @@ EXPORTED_SYMBOLS = (
     "fs_digest_batch_fcs",
     "fs_digest_batch_multi",
     "fs_ctx_set_kernel",
+    "fs_ctx_last_kernel",
     "fs_host_alloc",
     "fs_host_free",
     "fs_group_create",
@@ -123,6 +124,8 @@ def load_library() -> ctypes.CDLL:
     lib.fs_digest_batch_fcs.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp]
     lib.fs_digest_batch_fcs.restype = ctypes.c_int32
     lib.fs_ctx_set_kernel.argtypes = [vp, ctypes.c_int]
+    lib.fs_ctx_last_kernel.argtypes = [vp]
+    lib.fs_ctx_last_kernel.restype = ctypes.c_int
     lib.fs_digest_batch_multi.restype = i32
     lib.fs_digest_batch_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, u64, vp, vp, u32, u32, vp, vp]
     lib.fs_host_alloc.restype = i32
@@ -203,6 +206,15 @@ class Engine:
         kernel (256-byte rows, frames ordered by length into passes); 4: the one-pass kernel with
         block-aligned rows; 5: the same as two 8-wave workgroups per CU (RX ops)."""
         self._check(self.lib.fs_ctx_set_kernel(self._ctx, int(variant)), "fs_ctx_set_kernel")
+
+    def last_kernel(self) -> int:
+        """The variant (1..5) this context's latest launch ran (0 before its first launch). With
+        variant 0 the first 16 launches run the mixed-length kernel (2); it stays chosen while its
+        batches have mixed-length tiles, uniform traffic then moves to the one-pass kernel (4)."""
+        v = self.lib.fs_ctx_last_kernel(self._ctx)
+        if v < 0:
+            self._check(v, "fs_ctx_last_kernel")
+        return int(v)
 
     # ---- device-resident path (torch tensors as device memory) -------------
     def digest_device(self, frames, offsets, lengths, mtu: int = 0, out=None, status=None, stream=None):

@@ -326,3 +326,37 @@ def test_many_tiles_per_wave(engine, n, flen):
         buf = rng.integers(0, 256, int(off[-1] + ln[-1] + 16), dtype=np.uint8)
         ln = ln.astype(np.int32)
     check(engine, buf, off, ln, label=f"many tiles n={n} len={flen}")
+
+
+def test_auto_choice_first_launches():
+    """Variant 0 (automatic): a fresh context's first launches run the mixed-length kernel, so a
+    mixed batch is fast from its first call (the one-pass kernel's report would reach the host
+    launches late); it stays chosen while its own batches have mode-B tiles, and uniform traffic
+    moves to the block-aligned one-pass kernel once the initial window (16 launches) ends.
+    Results are the same either way (checked against the oracle after each switch)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    e = Engine(0)
+    try:
+        assert e.last_kernel() == 0
+        buf, off, ln = synth.mixed_batch(4096, seed=5)
+        check(e, buf, off, ln, label="first mixed launch")
+        assert e.last_kernel() == Engine.KERNEL_MIXED
+        for _ in range(40):
+            run_device(e, buf, off, ln)
+        assert e.last_kernel() == Engine.KERNEL_MIXED  # sticky through its own reports
+        check(e, buf, off, ln, label="mixed traffic")
+    finally:
+        e.close()
+    e = Engine(0)
+    try:
+        buf, off, ln = synth.uniform_batch(4096, 1500, seed=6)
+        kinds = []
+        for _ in range(24):
+            run_device(e, buf, off, ln)
+            kinds.append(e.last_kernel())
+        assert kinds[:16] == [Engine.KERNEL_MIXED] * 16 and kinds[16:] == [Engine.KERNEL_ALIGNED] * 8, kinds
+        check(e, buf, off, ln, label="uniform traffic after the window")
+        assert e.last_kernel() == Engine.KERNEL_ALIGNED
+    finally:
+        e.close()
