@@ -18,11 +18,12 @@
 using framesum::FsTables;
 
 // Host-staged path: the batch is cut into chunks of about kChunkBytes of frame bytes,
-// staged through kHostSlots device buffers. All H2D copies go back to back on one copy
-// stream (one DMA engine streaming the PCIe link); kernels and the small D2H copies run
-// on a compute stream. Events order each chunk's kernel after its copy (`copied`) and
-// the reuse of a slot by chunk c + kHostSlots after chunk c's kernel (`consumed`), so
-// chunk c+1's H2D overlaps chunk c's kernel and D2H.
+// staged through kHostSlots device buffers. The whole batch's descriptors go first, in one
+// H2D copy; the chunks' frame bytes then alternate between two copy streams (two DMA queues
+// keep the PCIe link busier than one: no gap between one chunk's copy and the next); kernels
+// and the small D2H copies run on a compute stream. Events order each chunk's kernel after
+// its copy (`copied`) and the reuse of a slot by chunk c + kHostSlots after chunk c's kernel
+// (`consumed`), so chunk c+1's H2D overlaps chunk c's kernel and D2H.
 constexpr int kHostSlots = 3;
 constexpr uint64_t kChunkBytes = 16ull << 20;
 constexpr uint32_t kChunkFrames = 1u << 20;
@@ -52,6 +53,10 @@ struct fs_ctx {
     int force_kernel = 0;  // fs_ctx_set_kernel
     HostSlot slot[kHostSlots];
     hipStream_t copy_stream = nullptr, compute_stream = nullptr;
+    hipStream_t copy_stream2 = nullptr;  // the odd chunks' frame copies
+    hipEvent_t desc_copied = nullptr;    // the batch's descriptors are on the device
+    uint8_t* d_desc = nullptr;           // the batch's offsets (8 n) then lengths (4 n)
+    uint64_t cap_desc_n = 0;
     // pinned host mirrors of the descriptors and results, so every per-chunk copy is
     // asynchronous even when the caller's arrays are pageable (Go slices, numpy)
     uint8_t* h_pin = nullptr;
@@ -110,6 +115,16 @@ fs_status ensure_slot(fs_ctx* ctx, HostSlot& sl, uint64_t frame_bytes, uint32_t 
 }
 
 // h_pin layout for n frames: offsets (8n) | lengths (4n) | digests (8n) | status (n)
+fs_status ensure_desc(fs_ctx* ctx, uint32_t n) {
+    if (n <= ctx->cap_desc_n) return FS_SUCCESS;
+    (void)hipFree(ctx->d_desc);  // the previous call's kernels have ended (callers synchronize first)
+    ctx->d_desc = nullptr;
+    ctx->cap_desc_n = 0;
+    if (hipMalloc(&ctx->d_desc, (size_t)n * 12 + 64) != hipSuccess) return set_err(ctx, FS_E_NOMEM, "hipMalloc descriptors");
+    ctx->cap_desc_n = n;
+    return FS_SUCCESS;
+}
+
 fs_status ensure_pinned(fs_ctx* ctx, uint32_t n) {
     if (n <= ctx->cap_pin_n) return FS_SUCCESS;
     if (ctx->h_pin) FS_HIP(ctx, hipHostFree(ctx->h_pin));
@@ -180,6 +195,8 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->compute_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->desc_copied, hipEventDisableTiming);
     for (int k = 0; k < kHostSlots && e == hipSuccess; ++k) {
         e = hipEventCreateWithFlags(&ctx->slot[k].copied, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->slot[k].consumed, hipEventDisableTiming);
@@ -200,6 +217,10 @@ fs_status fs_ctx_destroy(fs_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
     if (ctx->compute_stream) (void)hipStreamSynchronize(ctx->compute_stream);
+    if (ctx->copy_stream2) (void)hipStreamSynchronize(ctx->copy_stream2);
+    if (ctx->copy_stream2) (void)hipStreamDestroy(ctx->copy_stream2);
+    if (ctx->desc_copied) (void)hipEventDestroy(ctx->desc_copied);
+    (void)hipFree(ctx->d_desc);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->compute_stream) (void)hipStreamDestroy(ctx->compute_stream);
     for (HostSlot& sl : ctx->slot) {
@@ -285,6 +306,8 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));  // the pinned mirrors are free
     fs_status pst = ensure_pinned(ctx, n);
     if (pst != FS_SUCCESS) return pst;
+    pst = ensure_desc(ctx, n);
+    if (pst != FS_SUCCESS) return pst;
     uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pin);
     uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pin + (size_t)n * 8);
     fs_digest* h_out = reinterpret_cast<fs_digest*>(ctx->h_pin + (size_t)n * 12);
@@ -297,6 +320,12 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     } catch (const std::bad_alloc&) {
         return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: out of host memory");
     }
+    // the batch's descriptors in one copy (h_off and h_len are contiguous in the pinned mirror)
+    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(ctx->d_desc);
+    const uint32_t* d_len = reinterpret_cast<const uint32_t*>(ctx->d_desc + (size_t)n * 8);
+    FS_HIP(ctx, hipMemcpyAsync(ctx->d_desc, h_off, (size_t)n * 12, hipMemcpyHostToDevice, ctx->copy_stream));
+    FS_HIP(ctx, hipEventRecord(ctx->desc_copied, ctx->copy_stream));
+    FS_HIP(ctx, hipStreamWaitEvent(ctx->compute_stream, ctx->desc_copied, 0));
     for (size_t chunk = 0; chunk < chunks.size(); ++chunk) {
         const uint32_t c0 = chunks[chunk].c0, c1 = chunks[chunk].c1;
         const uint64_t cpy_lo = chunks[chunk].cpy_lo, cpy_hi = chunks[chunk].cpy_hi;
@@ -304,16 +333,14 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         const uint32_t cnt = c1 - c0;
         fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, cnt);
         if (st != FS_SUCCESS) return st;
-        const hipStream_t cs = ctx->copy_stream, ks = ctx->compute_stream;
+        const hipStream_t cs = (chunk & 1u) ? ctx->copy_stream2 : ctx->copy_stream, ks = ctx->compute_stream;
         if (sl.used) FS_HIP(ctx, hipStreamWaitEvent(cs, sl.consumed, 0));  // chunk c - kHostSlots done with it
         FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, cs));
-        FS_HIP(ctx, hipMemcpyAsync(sl.d_offsets, h_off + c0, (size_t)cnt * 8, hipMemcpyHostToDevice, cs));
-        FS_HIP(ctx, hipMemcpyAsync(sl.d_lengths, h_len + c0, (size_t)cnt * 4, hipMemcpyHostToDevice, cs));
         FS_HIP(ctx, hipEventRecord(sl.copied, cs));
         FS_HIP(ctx, hipStreamWaitEvent(ks, sl.copied, 0));
         // the kernel addresses frame i at base + offsets[i]: base = staging - cpy_lo (4-B aligned)
         const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
-        FS_HIP(ctx, framesum::launch_digest(base, sl.d_offsets, sl.d_lengths, cnt, mtu, ctx->d_tables, sl.d_out,
+        FS_HIP(ctx, framesum::launch_digest(base, d_off + c0, d_len + c0, cnt, mtu, ctx->d_tables, sl.d_out,
                                             status ? sl.d_status : nullptr, ks, ctx->num_cus, ctx->h_report,
                                             ctx->d_report, ctx->force_kernel, framesum::FsOp::kDigest, nullptr, 0, ctx->d_tables_w));
         FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
