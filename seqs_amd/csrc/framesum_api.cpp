@@ -31,7 +31,7 @@ constexpr uint32_t kChunkFrames = 1u << 20;
 constexpr uint32_t kMaxFrames = 1u << 31;
 
 struct HostSlot {
-    hipEvent_t copied = nullptr, consumed = nullptr;
+    hipEvent_t copied = nullptr, consumed = nullptr, landed = nullptr;  // landed: the chunk's results are in the mirror
     bool used = false;
     uint8_t* d_frames = nullptr;
     uint64_t cap_frames = 0;
@@ -200,6 +200,7 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
     for (int k = 0; k < kHostSlots && e == hipSuccess; ++k) {
         e = hipEventCreateWithFlags(&ctx->slot[k].copied, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->slot[k].consumed, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->slot[k].landed, hipEventDisableTiming);
     }
     delete h;
     if (e != hipSuccess) {
@@ -226,6 +227,7 @@ fs_status fs_ctx_destroy(fs_ctx* ctx) {
     for (HostSlot& sl : ctx->slot) {
         if (sl.copied) (void)hipEventDestroy(sl.copied);
         if (sl.consumed) (void)hipEventDestroy(sl.consumed);
+        if (sl.landed) (void)hipEventDestroy(sl.landed);
         (void)hipFree(sl.d_frames);
         (void)hipFree(sl.d_offsets);
         (void)hipFree(sl.d_lengths);
@@ -312,31 +314,54 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pin + (size_t)n * 8);
     fs_digest* h_out = reinterpret_cast<fs_digest*>(ctx->h_pin + (size_t)n * 12);
     uint8_t* h_st = ctx->h_pin + (size_t)n * 20;
-    std::memcpy(h_off, offsets, (size_t)n * 8);
-    std::memcpy(h_len, lengths, (size_t)n * 4);
     std::vector<framesum::plan::Chunk> chunks;
     try {
         framesum::plan::host_chunks(offsets, lengths, n, frames_bytes, kChunkBytes, kChunkFrames, chunks);
     } catch (const std::bad_alloc&) {
         return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: out of host memory");
     }
-    // the batch's descriptors in one copy (h_off and h_len are contiguous in the pinned mirror)
+    const hipStream_t ks = ctx->compute_stream;
+    // chunk k's frame bytes into its slot, on copy stream k & 1 (once the slot's previous chunk
+    // has been consumed by its kernel)
+    auto copy_chunk = [&](size_t k) -> fs_status {
+        const framesum::plan::Chunk& c = chunks[k];
+        HostSlot& sl = ctx->slot[k % kHostSlots];
+        fs_status st = ensure_slot(ctx, sl, c.cpy_hi - c.cpy_lo + 64, c.c1 - c.c0);
+        if (st != FS_SUCCESS) return st;
+        const hipStream_t cs = (k & 1u) ? ctx->copy_stream2 : ctx->copy_stream;
+        if (sl.used) FS_HIP(ctx, hipStreamWaitEvent(cs, sl.consumed, 0));  // chunk k - kHostSlots done with it
+        FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + c.cpy_lo, c.cpy_hi - c.cpy_lo, hipMemcpyHostToDevice, cs));
+        FS_HIP(ctx, hipEventRecord(sl.copied, cs));
+        return FS_SUCCESS;
+    };
+    // chunk k's results from the pinned mirror into the caller's arrays, once they have landed
+    auto deliver = [&](size_t k) -> fs_status {
+        const framesum::plan::Chunk& c = chunks[k];
+        FS_HIP(ctx, hipEventSynchronize(ctx->slot[k % kHostSlots].landed));
+        std::memcpy(out + c.c0, h_out + c.c0, (size_t)(c.c1 - c.c0) * sizeof(fs_digest));
+        if (status) std::memcpy(status + c.c0, h_st + c.c0, c.c1 - c.c0);
+        return FS_SUCCESS;
+    };
+    // the first chunk's frames stream while the descriptors are mirrored (pinned) and then
+    // copied, all of them in one copy (h_off and h_len are contiguous in the mirror)
+    fs_status st = copy_chunk(0);
+    if (st != FS_SUCCESS) return st;
+    std::memcpy(h_off, offsets, (size_t)n * 8);
+    std::memcpy(h_len, lengths, (size_t)n * 4);
     const uint64_t* d_off = reinterpret_cast<const uint64_t*>(ctx->d_desc);
     const uint32_t* d_len = reinterpret_cast<const uint32_t*>(ctx->d_desc + (size_t)n * 8);
-    FS_HIP(ctx, hipMemcpyAsync(ctx->d_desc, h_off, (size_t)n * 12, hipMemcpyHostToDevice, ctx->copy_stream));
-    FS_HIP(ctx, hipEventRecord(ctx->desc_copied, ctx->copy_stream));
-    FS_HIP(ctx, hipStreamWaitEvent(ctx->compute_stream, ctx->desc_copied, 0));
+    FS_HIP(ctx, hipMemcpyAsync(ctx->d_desc, h_off, (size_t)n * 12, hipMemcpyHostToDevice, ctx->copy_stream2));
+    FS_HIP(ctx, hipEventRecord(ctx->desc_copied, ctx->copy_stream2));
+    FS_HIP(ctx, hipStreamWaitEvent(ks, ctx->desc_copied, 0));
     for (size_t chunk = 0; chunk < chunks.size(); ++chunk) {
         const uint32_t c0 = chunks[chunk].c0, c1 = chunks[chunk].c1;
-        const uint64_t cpy_lo = chunks[chunk].cpy_lo, cpy_hi = chunks[chunk].cpy_hi;
+        const uint64_t cpy_lo = chunks[chunk].cpy_lo;
         HostSlot& sl = ctx->slot[chunk % kHostSlots];
         const uint32_t cnt = c1 - c0;
-        fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, cnt);
-        if (st != FS_SUCCESS) return st;
-        const hipStream_t cs = (chunk & 1u) ? ctx->copy_stream2 : ctx->copy_stream, ks = ctx->compute_stream;
-        if (sl.used) FS_HIP(ctx, hipStreamWaitEvent(cs, sl.consumed, 0));  // chunk c - kHostSlots done with it
-        FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, cs));
-        FS_HIP(ctx, hipEventRecord(sl.copied, cs));
+        if (chunk > 0) {
+            st = copy_chunk(chunk);
+            if (st != FS_SUCCESS) return st;
+        }
         FS_HIP(ctx, hipStreamWaitEvent(ks, sl.copied, 0));
         // the kernel addresses frame i at base + offsets[i]: base = staging - cpy_lo (4-B aligned)
         const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
@@ -347,10 +372,18 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         sl.used = true;
         FS_HIP(ctx, hipMemcpyAsync(h_out + c0, sl.d_out, (size_t)cnt * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
         if (status) FS_HIP(ctx, hipMemcpyAsync(h_st + c0, sl.d_status, cnt, hipMemcpyDeviceToHost, ks));
+        FS_HIP(ctx, hipEventRecord(sl.landed, ks));
+        // chunk - 2's results while this one streams (its slot's `landed` is re-recorded by chunk + 1)
+        if (chunk >= 2) {
+            st = deliver(chunk - 2);
+            if (st != FS_SUCCESS) return st;
+        }
     }
-    FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));
-    std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
-    if (status) std::memcpy(status, h_st, n);
+    for (size_t k = chunks.size() >= 2 ? chunks.size() - 2 : 0; k < chunks.size(); ++k) {
+        st = deliver(k);
+        if (st != FS_SUCCESS) return st;
+    }
+    FS_HIP(ctx, hipStreamSynchronize(ks));
     return FS_SUCCESS;
 }
 
