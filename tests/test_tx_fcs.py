@@ -254,3 +254,32 @@ def test_gpu_fill_host_and_calculate_headers(engine):
         assert g == pyref.fill_frame(f, 0, FILL_CSUM | FCS_APPEND)[0]
     with pytest.raises(Exception):
         engine.fill_host(np.zeros(100, np.uint8), np.array([90], np.uint64), np.array([8], np.uint32), 0, FCS_APPEND)
+
+
+@pytest.mark.gpu
+def test_gpu_fill_host_large(engine):
+    # the host-staged fill of a batch spanning several 16-MiB chunks, from pinned and pageable
+    # memory: byte-for-byte equal to the oracle's fill, stale checksum fields and the noise
+    # between frames included
+    from seqs_amd import synth
+
+    n, flen, room = 28000, 1500, 4
+    src, soff, _ = synth.uniform_batch(n, flen, seed=11)
+    rng = np.random.default_rng(12)
+    off = np.arange(n, dtype=np.int64) * (flen + room + 2)  # 2-B phase steps: every alignment
+    buf = rng.integers(0, 256, int(off[-1] + flen + room + 64), dtype=np.uint8)
+    idx = off[:, None] + np.arange(flen)[None, :]
+    buf[idx] = src[soff[:, None] + np.arange(flen)[None, :]]
+    buf[off[:, None] + np.array([24, 25, 50, 51])[None, :]] = rng.integers(0, 256, (n, 4), dtype=np.uint8)
+    ln = np.full(n, flen, dtype=np.int32)
+    assert int(off[-1]) > 2 * (16 << 20)
+    ebuf = buf.copy()
+    edig, est = coracle.fill_batch(ebuf, off, ln, 0, FILL_CSUM | FCS_APPEND)
+    torch = pytest.importorskip("torch")
+    for pinned in (True, False):
+        host = torch.empty(buf.size, dtype=torch.uint8).pin_memory().numpy() if pinned else np.empty_like(buf)
+        host[:] = buf
+        dig, st = engine.fill_host(host, off, ln, 0, FILL_CSUM | FCS_APPEND)
+        assert np.array_equal(dig, edig) and np.array_equal(st, est), pinned
+        assert (st == 0).all()
+        assert np.array_equal(host, ebuf), pinned
