@@ -27,14 +27,21 @@ KERNEL = "digest_kernel"
 
 
 def counters(pass_dir):
-    per = {}
+    # only the kernel the run chose most often (a context's first launches run the mixed-length
+    # kernel whatever the batch: the automatic choice's initial window)
+    rows = []
     for path in glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
-            for row in csv.DictReader(f):
-                if KERNEL not in row["Kernel_Name"]:
-                    continue
-                key = (row["Counter_Name"], row["Dispatch_Id"])
-                per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+            rows += [r for r in csv.DictReader(f) if KERNEL in r["Kernel_Name"]]
+    names = {}
+    for r in rows:
+        names.setdefault(r["Kernel_Name"], set()).add(r["Dispatch_Id"])
+    main = max(names, key=lambda k: len(names[k])) if names else None
+    per = {}
+    for row in rows:
+        if row["Kernel_Name"] == main:
+            key = (row["Counter_Name"], row["Dispatch_Id"])
+            per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
     by_name = {}
     for (name, _), v in per.items():
         by_name.setdefault(name, []).append(v)
