@@ -306,6 +306,9 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(bad) + " ends past frames_bytes");
     FS_HIP(ctx, hipSetDevice(ctx->device));
     FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));  // the pinned mirrors are free
+    // (and no copy of a call that failed half-way is still writing a slot)
+    FS_HIP(ctx, hipStreamSynchronize(ctx->copy_stream));
+    FS_HIP(ctx, hipStreamSynchronize(ctx->copy_stream2));
     fs_status pst = ensure_pinned(ctx, n);
     if (pst != FS_SUCCESS) return pst;
     pst = ensure_desc(ctx, n);
