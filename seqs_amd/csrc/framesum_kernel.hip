@@ -1567,6 +1567,12 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         else if (w == 1u) __builtin_amdgcn_s_setprio(1);
     } else if (FS_AGE_PRIO == 2) {  // two levels: the SIMD's younger half (waves 8..15) outranks the older
         if ((__builtin_amdgcn_readfirstlane(wave) >> 3) != 0u) __builtin_amdgcn_s_setprio(1);
+    } else if (FS_AGE_PRIO == 3) {  // (experiment) the SIMD's youngest wave (12..15) only
+        if ((__builtin_amdgcn_readfirstlane(wave) >> 2) == 3u) __builtin_amdgcn_s_setprio(1);
+    } else if (FS_AGE_PRIO == 4) {  // (experiment) three levels: 0, 1, 1, 2
+        const uint32_t w = __builtin_amdgcn_readfirstlane(wave) >> 2;
+        if (w == 3u) __builtin_amdgcn_s_setprio(2);
+        else if (w != 0u) __builtin_amdgcn_s_setprio(1);
     }
     FS_STAMP(1);
 
