@@ -111,6 +111,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_AB_ROWS_FIRST
 #define FS_AB_ROWS_FIRST 1  // mixed-length kernel: the first tile's rows before its header DMA
 #endif
+#ifndef FS_FIN_PRIO
+#define FS_FIN_PRIO 0  // one-pass kernel: s_setprio(3) for the combine and the finish
+#endif
 #ifndef FS_PLAIN_VALU
 #define FS_PLAIN_VALU 1  // the plain tables built in place by VALU from their bases (0: copied by LDS-DMA)
 #endif
@@ -1709,6 +1712,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         } else {
             parse(false);  // no rows (every frame of the tile under 4 bytes): rejected by length
         }
+        if (FS_FIN_PRIO) __builtin_amdgcn_s_setprio(3);  // (experiment) the combine and finish outrank row loops
         FS_STAMP(2);
 
         // ---- combine the 16 streams of each frame: C = Z_(4-t)( xor_l Z_16(3-l)( U_l ) ),
