@@ -124,8 +124,11 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_PRIO_MIN
 #define FS_PRIO_MIN 36  // ... for tiles of more rows than this
 #endif
+#ifndef FS_PRIO_AB
+#define FS_PRIO_AB 0  // ... in the mixed-length kernel (round 2: off, C3 -0.6 us alone and +1.6% whole job)
+#endif
 #ifndef FS_PRIO
-#define FS_PRIO 1  // progress-based s_setprio per block of rows
+#define FS_PRIO 1  // progress-based s_setprio per block of rows (one-pass kernel)
 #endif
 
 constexpr int kWave = 64;
@@ -1892,7 +1895,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             auto prio = [&](int r0) {
                 // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
                 // a wave with more rows left gets a higher priority.
-                if (FS_PRIO && total_rows > 36) {  // long tiles only (C2-size tiles run faster without)
+                if (FS_PRIO_AB && total_rows > 36) {  // long tiles only (C2-size tiles run faster without)
                     const int left4 = 4 * (total_rows - done0 - r0);  // vs quarters of total_rows
                     if (left4 > 3 * total_rows) __builtin_amdgcn_s_setprio(3);
                     else if (left4 > 2 * total_rows) __builtin_amdgcn_s_setprio(2);
