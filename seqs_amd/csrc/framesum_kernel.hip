@@ -124,6 +124,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 #ifndef FS_PRIO_MIN
 #define FS_PRIO_MIN 36  // ... for tiles of more rows than this
 #endif
+#ifndef FS_AGE_PRIO_AB
+#define FS_AGE_PRIO_AB 2  // mixed-length kernel: 2 = the one-pass kernel's two-level age priority (C3 whole job +2.6%)
+#endif
 #ifndef FS_PRIO_AB
 #define FS_PRIO_AB 0  // ... in the mixed-length kernel (round 2: off, C3 -0.6 us alone and +1.6% whole job)
 #endif
@@ -1861,6 +1864,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     tables_landed<kPrefetch>(first, U.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    if (FS_AGE_PRIO_AB == 2 && (wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // the SIMD's younger half first
     FS_STAMP(1);
 
     while (tile < ntiles) {
