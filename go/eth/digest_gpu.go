@@ -270,3 +270,83 @@ func (m *GPUs) DigestBatch(frames [][]byte, mtu uint16, out []Digest, verdicts [
 	}
 	return nil
 }
+
+// Group drives several GPUs of this host from one process with device-resident shards and RCCL
+// (fs_group_create / fs_digest_batch_sharded; BASELINE configs[3]): frames that the NIC placed in
+// the HBM of several GPUs (GPUDirect RDMA) are digested where they lie, round-robin sharded
+// (global frame i is frame i / N of shard i % N; eth/crc.go:12-17: CRC791 is per call, so frames
+// are independent); only the 8-byte digests and 1-byte verdicts travel, over xGMI, to the first
+// device (ncclGather), where a de-interleave kernel restores global order. The consumer is the
+// same as DigestBatch's: stacks.PortStack.RecvEth (stacks/portstack.go:163) -> :240 / :303.
+type Group struct {
+	g    *C.fs_group
+	n    int
+	ptrs unsafe.Pointer // C memory: frames, offsets, lengths pointer arrays of n entries each
+}
+
+// DeviceShard is shard k of a sharded batch: DEVICE pointers on the group's k-th device, laid
+// out as fs_digest_batch expects (frame i = Frames[Offsets[i] : Offsets[i]+Lengths[i]]), holding
+// ShardCount(n, N, k) frames. The memory is the caller's (e.g. its NIC driver's receive rings).
+type DeviceShard struct {
+	Frames  unsafe.Pointer // uint8
+	Offsets unsafe.Pointer // uint64 per frame
+	Lengths unsafe.Pointer // uint32 per frame
+}
+
+// OpenGroup creates one context, one stream and one RCCL communicator per listed device
+// (distinct devices; ncclCommInitAll).
+func OpenGroup(devices []int) (*Group, error) {
+	if len(devices) == 0 {
+		return nil, errors.New("framesum: no devices")
+	}
+	devs := (*C.int)(C.malloc(C.size_t(len(devices)) * C.size_t(unsafe.Sizeof(C.int(0)))))
+	defer C.free(unsafe.Pointer(devs))
+	arr := unsafe.Slice(devs, len(devices))
+	for i, d := range devices {
+		arr[i] = C.int(d)
+	}
+	var g *C.fs_group
+	if st := C.fs_group_create(devs, C.int(len(devices)), &g); st != C.FS_SUCCESS {
+		return nil, errors.New("framesum: " + C.GoString(C.fs_group_last_error(nil)))
+	}
+	ptrs := C.malloc(3 * C.size_t(len(devices)) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	return &Group{g: g, n: len(devices), ptrs: ptrs}, nil
+}
+
+// Close releases the group's contexts, streams and communicators.
+func (g *Group) Close() error {
+	if g.g == nil {
+		return nil
+	}
+	C.fs_group_destroy(g.g)
+	C.free(g.ptrs)
+	g.g, g.ptrs = nil, nil
+	return nil
+}
+
+// ShardCount is the number of frames shard `shard` holds when n global frames go round-robin
+// over nshards shards (fs_shard_count).
+func ShardCount(n uint64, nshards, shard int) uint64 {
+	return uint64(C.fs_shard_count(C.uint64_t(n), C.uint32_t(nshards), C.uint32_t(shard)))
+}
+
+// DigestSharded digests a global batch of n frames held as one DeviceShard per group device.
+// out (n Digests, 8 bytes each) and verdicts (n bytes; nil to skip) are DEVICE pointers on the
+// group's first device and receive the results in global frame order. It returns when they are
+// written.
+func (g *Group) DigestSharded(shards []DeviceShard, n uint64, mtu uint16, out, verdicts unsafe.Pointer) error {
+	if len(shards) != g.n {
+		return errors.New("framesum: one DeviceShard per group device")
+	}
+	p := unsafe.Slice((*unsafe.Pointer)(g.ptrs), 3*g.n)
+	for k, s := range shards {
+		p[k], p[g.n+k], p[2*g.n+k] = s.Frames, s.Offsets, s.Lengths
+	}
+	st := C.fs_digest_batch_sharded(g.g, (**C.uint8_t)(unsafe.Pointer(&p[0])),
+		(**C.uint64_t)(unsafe.Pointer(&p[g.n])), (**C.uint32_t)(unsafe.Pointer(&p[2*g.n])),
+		C.uint64_t(n), C.uint32_t(mtu), (*C.fs_digest)(out), (*C.uint8_t)(verdicts))
+	if st != C.FS_SUCCESS {
+		return errors.New("framesum: " + C.GoString(C.fs_group_last_error(g.g)))
+	}
+	return nil
+}

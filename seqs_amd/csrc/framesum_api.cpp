@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <system_error>
@@ -47,6 +48,11 @@ struct fs_ctx {
     int num_cus = 0;
     FsTables* d_tables = nullptr;
     framesum::FsTablesW* d_tables_w = nullptr;
+    framesum::FsTablesRx* d_tables_rx = nullptr;
+    int rx_grid = 1;  // streaming kernel: workgroups per CU (FS_RX_GRID)
+    // fault injection for the host-staged pipeline's tests (FS_FAULT_CHUNK=k: fs_digest_batch_host
+    // fails with FS_E_NOMEM at chunk k, after the earlier chunks' work and chunk k's copy are queued)
+    long fault_chunk = -1;
     // host-mapped word the kernels set when a batch has widely mixed lengths (launch_digest)
     volatile uint32_t* h_report = nullptr;
     uint32_t* d_report = nullptr;
@@ -136,6 +142,28 @@ fs_status ensure_pinned(fs_ctx* ctx, uint32_t n) {
     return FS_SUCCESS;
 }
 
+// Every host-staged entry point starts here: the pinned mirrors and the staging slots are free
+// only once the context's compute stream AND both copy streams are idle (a host-staged call that
+// failed half-way may have left odd-chunk copies in flight on copy_stream2 that would otherwise
+// write a slot while the next call stages into it).
+fs_status quiesce_host_streams(fs_ctx* ctx) {
+    FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));
+    FS_HIP(ctx, hipStreamSynchronize(ctx->copy_stream));
+    FS_HIP(ctx, hipStreamSynchronize(ctx->copy_stream2));
+    return FS_SUCCESS;
+}
+
+// One launch of the context's kernel choice (variant 6: the streaming kernel).
+hipError_t launch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                  uint32_t mtu, fs_digest* out, uint8_t* status, hipStream_t stream, framesum::FsOp op,
+                  uint8_t* wframes, uint32_t tx) {
+    if (ctx->force_kernel == 6)
+        return framesum::launch_rx(frames, offsets, lengths, n, mtu, ctx->d_tables_rx, out, status, stream, ctx->num_cus,
+                                   ctx->rx_grid, (int)op, wframes, tx);
+    return framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status, stream, ctx->num_cus,
+                                   ctx->h_report, ctx->d_report, ctx->force_kernel, op, wframes, tx, ctx->d_tables_w);
+}
+
 }  // namespace
 
 extern "C" {
@@ -181,6 +209,16 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
         if (e == hipSuccess) e = hipMalloc(&ctx->d_tables_w, sizeof(framesum::FsTablesW));
         if (e == hipSuccess) e = hipMemcpy(ctx->d_tables_w, hw, sizeof(framesum::FsTablesW), hipMemcpyHostToDevice);
         delete hw;
+    }
+    if (e == hipSuccess) {
+        framesum::FsTablesRx hr;
+        framesum::build_tables_rx(&hr);
+        e = hipMalloc(&ctx->d_tables_rx, sizeof(framesum::FsTablesRx));
+        if (e == hipSuccess) e = hipMemcpy(ctx->d_tables_rx, &hr, sizeof(framesum::FsTablesRx), hipMemcpyHostToDevice);
+        const char* g = std::getenv("FS_RX_GRID");
+        if (g && std::atoi(g) == 2) ctx->rx_grid = 2;
+        const char* fc = std::getenv("FS_FAULT_CHUNK");
+        if (fc && *fc) ctx->fault_chunk = std::atol(fc);
     }
     if (e == hipSuccess) {
         void* hp = nullptr;
@@ -238,6 +276,7 @@ fs_status fs_ctx_destroy(fs_ctx* ctx) {
     if (ctx->h_report) (void)hipHostFree(const_cast<uint32_t*>(ctx->h_report));
     (void)hipFree(ctx->d_tables);
     (void)hipFree(ctx->d_tables_w);
+    (void)hipFree(ctx->d_tables_rx);
     delete ctx;
     return FS_SUCCESS;
 }
@@ -254,9 +293,7 @@ fs_status fs_digest_batch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* of
     if (reinterpret_cast<uintptr_t>(frames) & 3u)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch: frames must be 4-byte aligned");
     FS_HIP(ctx, hipSetDevice(ctx->device));
-    FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
-                                        reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
-                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kDigest, nullptr, 0, ctx->d_tables_w));
+    FS_HIP(ctx, launch(ctx, frames, offsets, lengths, n, mtu, out, status, reinterpret_cast<hipStream_t>(stream), framesum::FsOp::kDigest, nullptr, 0));
     return FS_SUCCESS;
 }
 
@@ -271,9 +308,7 @@ fs_status fs_fill_batch(fs_ctx* ctx, uint8_t* frames, const uint64_t* offsets, c
     if (reinterpret_cast<uintptr_t>(frames) & 3u)
         return set_err(ctx, FS_E_INVALID, "fs_fill_batch: frames must be 4-byte aligned");
     FS_HIP(ctx, hipSetDevice(ctx->device));
-    FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
-                                        reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
-                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFill, frames, flags, ctx->d_tables_w));
+    FS_HIP(ctx, launch(ctx, frames, offsets, lengths, n, mtu, out, status, reinterpret_cast<hipStream_t>(stream), framesum::FsOp::kFill, frames, flags));
     return FS_SUCCESS;
 }
 
@@ -287,9 +322,7 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
     if (reinterpret_cast<uintptr_t>(frames) & 3u)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_fcs: frames must be 4-byte aligned");
     FS_HIP(ctx, hipSetDevice(ctx->device));
-    FS_HIP(ctx, framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status,
-                                        reinterpret_cast<hipStream_t>(stream), ctx->num_cus, ctx->h_report,
-                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFcs, nullptr, 0, ctx->d_tables_w));
+    FS_HIP(ctx, launch(ctx, frames, offsets, lengths, n, mtu, out, status, reinterpret_cast<hipStream_t>(stream), framesum::FsOp::kFcs, nullptr, 0));
     return FS_SUCCESS;
 }
 
@@ -305,11 +338,9 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     if (bad < n)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(bad) + " ends past frames_bytes");
     FS_HIP(ctx, hipSetDevice(ctx->device));
-    FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));  // the pinned mirrors are free
-    // (and no copy of a call that failed half-way is still writing a slot)
-    FS_HIP(ctx, hipStreamSynchronize(ctx->copy_stream));
-    FS_HIP(ctx, hipStreamSynchronize(ctx->copy_stream2));
-    fs_status pst = ensure_pinned(ctx, n);
+    fs_status pst = quiesce_host_streams(ctx);
+    if (pst != FS_SUCCESS) return pst;
+    pst = ensure_pinned(ctx, n);
     if (pst != FS_SUCCESS) return pst;
     pst = ensure_desc(ctx, n);
     if (pst != FS_SUCCESS) return pst;
@@ -365,12 +396,13 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
             st = copy_chunk(chunk);
             if (st != FS_SUCCESS) return st;
         }
+        if ((long)chunk == ctx->fault_chunk)
+            return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: injected failure (FS_FAULT_CHUNK)");
         FS_HIP(ctx, hipStreamWaitEvent(ks, sl.copied, 0));
         // the kernel addresses frame i at base + offsets[i]: base = staging - cpy_lo (4-B aligned)
         const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
-        FS_HIP(ctx, framesum::launch_digest(base, d_off + c0, d_len + c0, cnt, mtu, ctx->d_tables, sl.d_out,
-                                            status ? sl.d_status : nullptr, ks, ctx->num_cus, ctx->h_report,
-                                            ctx->d_report, ctx->force_kernel, framesum::FsOp::kDigest, nullptr, 0, ctx->d_tables_w));
+        FS_HIP(ctx, launch(ctx, base, d_off + c0, d_len + c0, cnt, mtu, sl.d_out, status ? sl.d_status : nullptr, ks,
+                           framesum::FsOp::kDigest, nullptr, 0));
         FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
         sl.used = true;
         FS_HIP(ctx, hipMemcpyAsync(h_out + c0, sl.d_out, (size_t)cnt * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
@@ -413,8 +445,9 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
         hi = e > hi ? e : hi;
     }
     FS_HIP(ctx, hipSetDevice(ctx->device));
-    FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));
-    fs_status pst = ensure_pinned(ctx, n);
+    fs_status pst = quiesce_host_streams(ctx);
+    if (pst != FS_SUCCESS) return pst;
+    pst = ensure_pinned(ctx, n);
     if (pst != FS_SUCCESS) return pst;
     uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pin);
     uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pin + (size_t)n * 8);
@@ -433,9 +466,8 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
     FS_HIP(ctx, hipMemcpyAsync(sl.d_offsets, h_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
     FS_HIP(ctx, hipMemcpyAsync(sl.d_lengths, h_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
     uint8_t* base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
-    FS_HIP(ctx, framesum::launch_digest(base, sl.d_offsets, sl.d_lengths, n, mtu, ctx->d_tables, sl.d_out,
-                                        status ? sl.d_status : nullptr, ks, ctx->num_cus, ctx->h_report,
-                                        ctx->d_report, ctx->force_kernel, framesum::FsOp::kFill, base, flags, ctx->d_tables_w));
+    FS_HIP(ctx, launch(ctx, base, sl.d_offsets, sl.d_lengths, n, mtu, sl.d_out, status ? sl.d_status : nullptr, ks,
+                       framesum::FsOp::kFill, base, flags));
     FS_HIP(ctx, hipMemcpyAsync(frames + lo, sl.d_frames + (lo - cpy_lo), hi - lo, hipMemcpyDeviceToHost, ks));
     FS_HIP(ctx, hipMemcpyAsync(h_out, sl.d_out, (size_t)n * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
     if (status) FS_HIP(ctx, hipMemcpyAsync(h_st, sl.d_status, n, hipMemcpyDeviceToHost, ks));
@@ -555,7 +587,7 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
     ctx->err.clear();
-    if (variant < 0 || variant > 5) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0..5");
+    if (variant < 0 || variant > 6) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0..6");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
 }

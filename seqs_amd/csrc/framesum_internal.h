@@ -71,6 +71,25 @@ static_assert(offsetof(FsTablesW, basis) == kTablesWLdsBytes, "FsTablesW layout"
 
 void build_tables_w(FsTablesW* t);
 
+// The streaming kernel's tables (framesum_rx.hip). Each workgroup builds its 64-KB LDS image from
+// these bases (every table is GF(2)-linear in its byte): entry row e (256 B) holds, in dword slots
+// 0..31, Z_256[b][e] for slot 8b + c (8 copies per byte table: the row lookups are conflict-free),
+// and in slots 32..63 the 8 plain tables kRxPlain, T_t[b][e] at slot 32 + ((4t + b) ^ (e >> 3)).
+constexpr int kRxPlain[8] = {4, 16, 32, 48, 64, 128, 192, 1536};
+struct FsTablesRx {
+    uint32_t z256_basis[4][8];   // Z_256[b][1 << j]
+    uint32_t plain_basis[32][8]; // q = 4t + b: T_t[b][1 << j]
+};
+void build_tables_rx(FsTablesRx* t);
+// the LDS image those bases describe (host reference, for the CPU tests of the layout)
+void rx_region_image(const FsTablesRx* t, uint32_t region[256][64]);
+
+// Launch the streaming kernel (every operation). `grid_per_cu`: workgroups per CU (1 = one
+// 8-wave workgroup per CU, so consecutive launches co-reside; 2 = the whole CU for one launch).
+hipError_t launch_rx(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint32_t mtu,
+                     const FsTablesRx* tables, void* out, uint8_t* status, hipStream_t stream, int num_cus,
+                     int grid_per_cu, int op, uint8_t* wframes, uint32_t tx);
+
 // Launch the digest kernel. `num_cus` sizes the persistent grid. `report` (nullable) is a
 // host-mapped word: a kernel writes its launch id there when its batch has tiles of widely
 // mixed frame lengths; launches within a window after such a report use the kernel variant

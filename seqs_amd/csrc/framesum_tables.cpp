@@ -84,6 +84,38 @@ void build_tables(FsTables* t) {
     if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");
 }
 
+void build_tables_rx(FsTablesRx* t) {
+    std::memset(t, 0, sizeof(*t));
+    uint32_t t1[256];
+    byte_table(t1);
+    static uint32_t z[4][256];
+    op_table(t1, 256, z);
+    for (uint32_t b = 0; b < 4; ++b)
+        for (uint32_t j = 0; j < 8; ++j) t->z256_basis[b][j] = z[b][1u << j];
+    for (uint32_t k = 0; k < 8; ++k) {
+        op_table(t1, kRxPlain[k], z);
+        for (uint32_t b = 0; b < 4; ++b)
+            for (uint32_t j = 0; j < 8; ++j) t->plain_basis[4 * k + b][j] = z[b][1u << j];
+    }
+    // the standard byte table is Z_4's byte-3 table (the finish's tail bytes use it)
+    op_table(t1, 4, z);
+    if (std::memcmp(z[3], t1, sizeof(t1)) != 0) throw std::logic_error("Z_4 byte-3 table is not the CRC table");
+}
+
+void rx_region_image(const FsTablesRx* t, uint32_t region[256][64]) {
+    auto lin = [](const uint32_t basis[8], uint32_t e) {
+        uint32_t v = 0;
+        for (uint32_t j = 0; j < 8; ++j)
+            if ((e >> j) & 1u) v ^= basis[j];
+        return v;
+    };
+    for (uint32_t e = 0; e < 256; ++e) {
+        for (uint32_t b = 0; b < 4; ++b)
+            for (uint32_t c = 0; c < 8; ++c) region[e][8 * b + c] = lin(t->z256_basis[b], e);
+        for (uint32_t q = 0; q < 32; ++q) region[e][32u + (q ^ (e >> 3))] = lin(t->plain_basis[q], e);
+    }
+}
+
 void build_tables_w(FsTablesW* t) {
     std::memset(t, 0, sizeof(*t));
     uint32_t t1[256];

@@ -197,7 +197,7 @@ class Engine:
             raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
 
     # kernel variants (fs_ctx_set_kernel): results are identical, only the speed differs
-    KERNEL_AUTO, KERNEL_ONE_PASS, KERNEL_MIXED, KERNEL_WIDE, KERNEL_ALIGNED, KERNEL_DUAL = 0, 1, 2, 3, 4, 5
+    KERNEL_AUTO, KERNEL_ONE_PASS, KERNEL_MIXED, KERNEL_WIDE, KERNEL_ALIGNED, KERNEL_DUAL, KERNEL_STREAM = 0, 1, 2, 3, 4, 5, 6
 
     def set_kernel(self, variant: int) -> None:
         """0: automatic (the mixed-length kernel after a batch that had mixed-length tiles, the

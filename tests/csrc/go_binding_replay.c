@@ -5,16 +5,23 @@
  *   digest  GPU.DigestBatch   -> fs_digest_batch_host
  *   fill    GPU.FillBatch     -> fs_fill_batch_host, then the filled bytes copied back out
  *   multi   GPUs.DigestBatch  -> fs_digest_batch_multi over nctx contexts (all on device 0 here)
+ *   sharded Group.DigestSharded -> fs_group_create over every visible device, the batch sharded
+ *           round-robin into device memory (what the Go caller's NIC rings would hold; here
+ *           hipMalloc + hipMemcpy stand in), fs_digest_batch_sharded, results read back from the
+ *           first device
  * Input: a frame list file (u32 n, then n x {u32 len, len bytes}). Output: n fs_digest, n
  * verdict bytes, and for fill the filled frames as a frame list (len + 4 bytes with FCS).
  * tests/test_go_binding.py compares everything with the CPU oracle.
- * usage: go_binding_replay digest|fill|fill_fcs|multi <in.lst> <mtu> <out.bin> [nctx] */
+ * usage: go_binding_replay digest|fill|fill_fcs|multi|sharded <in.lst> <mtu> <out.bin> [nctx] */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "framesum.h"
+
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
 
 typedef struct {
     uint32_t n;
@@ -116,6 +123,77 @@ int main(int argc, char** argv) {
         st = fs_digest_batch_multi(ctxs, nctx, buf, total, g.offs, g.lens, fl.n, mtu, out, ver);
         for (int k = 1; k < nctx; ++k) fs_ctx_destroy(ctxs[k]);
         free(ctxs);
+    } else if (fl.n && !strcmp(mode, "sharded")) {
+        /* Group.DigestSharded: OpenGroup(devices), shard k = global frames k, k + N, ... packed
+         * 4-byte aligned into device k's memory, then one call; out/status on device 0 */
+        const int N = fs_device_count();
+        int* devs = calloc((size_t)N, sizeof(int));
+        for (int k = 0; k < N; ++k) devs[k] = k;
+        fs_group* grp = NULL;
+        if (fs_group_create(devs, N, &grp) != FS_SUCCESS) {
+            fprintf(stderr, "fs_group_create: %s\n", fs_group_last_error(NULL));
+            return 1;
+        }
+        const uint8_t** dfr = calloc((size_t)N, sizeof(void*));
+        const uint64_t** doff = calloc((size_t)N, sizeof(void*));
+        const uint32_t** dlen = calloc((size_t)N, sizeof(void*));
+        for (int k = 0; k < N; ++k) {
+            const uint64_t nk = fs_shard_count(fl.n, (uint32_t)N, (uint32_t)k);
+            uint64_t bytes = 16;
+            uint64_t* ho = calloc(nk + 1, 8);
+            uint32_t* hl = calloc(nk + 1, 4);
+            for (uint64_t j = 0; j < nk; ++j) {
+                const uint32_t i = (uint32_t)(j * (uint64_t)N + (uint64_t)k);
+                ho[j] = bytes - 16;
+                hl[j] = fl.len[i];
+                bytes += ((uint64_t)fl.len[i] + 3) & ~(uint64_t)3;
+            }
+            uint8_t* hb = calloc(bytes, 1);
+            for (uint64_t j = 0; j < nk; ++j) memcpy(hb + ho[j], fl.data[j * (uint64_t)N + (uint64_t)k], hl[j]);
+            void *df = NULL, *dof = NULL, *dl = NULL;
+            if (hipSetDevice(k) != hipSuccess || hipMalloc(&df, bytes) != hipSuccess ||
+                hipMalloc(&dof, 8 * (nk + 1)) != hipSuccess || hipMalloc(&dl, 4 * (nk + 1)) != hipSuccess ||
+                hipMemcpy(df, hb, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dof, ho, 8 * (nk + 1), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dl, hl, 4 * (nk + 1), hipMemcpyHostToDevice) != hipSuccess) {
+                fprintf(stderr, "device staging of shard %d failed\n", k);
+                return 1;
+            }
+            dfr[k] = df;
+            doff[k] = dof;
+            dlen[k] = dl;
+            free(hb);
+            free(ho);
+            free(hl);
+        }
+        void *dout = NULL, *dst = NULL;
+        if (hipSetDevice(0) != hipSuccess || hipMalloc(&dout, 8 * (size_t)fl.n) != hipSuccess ||
+            hipMalloc(&dst, fl.n) != hipSuccess) {
+            fprintf(stderr, "device output allocation failed\n");
+            return 1;
+        }
+        st = fs_digest_batch_sharded(grp, dfr, doff, dlen, fl.n, mtu, dout, dst);
+        if (st != FS_SUCCESS) {
+            fprintf(stderr, "sharded failed (%d): %s\n", st, fs_group_last_error(grp));
+            return 1;
+        }
+        if (hipMemcpy(out, dout, 8 * (size_t)fl.n, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(ver, dst, fl.n, hipMemcpyDeviceToHost) != hipSuccess) {
+            fprintf(stderr, "result copy failed\n");
+            return 1;
+        }
+        for (int k = 0; k < N; ++k) {
+            (void)hipSetDevice(k);
+            (void)hipFree((void*)dfr[k]);
+            (void)hipFree((void*)doff[k]);
+            (void)hipFree((void*)dlen[k]);
+        }
+        (void)hipSetDevice(0);
+        (void)hipFree(dout);
+        (void)hipFree(dst);
+        fs_group_destroy(grp);
+        free(devs);
+        printf("sharded over %d device(s)\n", N);
     }
     if (st != FS_SUCCESS) {
         fprintf(stderr, "%s failed (%d): %s\n", mode, st, fs_last_error(g.ctx));

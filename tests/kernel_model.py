@@ -316,3 +316,94 @@ def crc32_model_al(buf: bytes, S: int, length: int, base_phase: int = 0) -> int:
             Y ^= v
     t = (4 - (E & 3)) & 3
     return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
+
+
+# ---- the streaming kernel (seqs_amd/csrc/framesum_rx.hip) ---------------------------------
+Z256, Z1536, Z48, Z128, Z192 = op_table(256), op_table(1536), op_table(48), op_table(128), op_table(192)
+RX_PR, RX_PIECE = 6, 1536
+
+
+def rx_geometry(S: int, slen: int):
+    """(D, R, npc, h) of a frame as the streaming kernel cuts it (npc 0: bytewise)."""
+    E = S + slen
+    Ed, F4 = E & ~3, S & ~3
+    if slen < 4 or Ed < S + 4:
+        return 0, 0, 0, 0
+    D = (Ed - F4) // 4
+    R = (D + 63) // 64
+    npc = (R + RX_PR - 1) // RX_PR
+    return D, R, npc, R - RX_PR * (npc - 1)
+
+
+def crc32_model_rx(buf: bytes, S: int, slen: int, base: int = 0) -> int:
+    """CRC-32 of buf[S:S+slen] computed the way framesum_rx.hip does: end-anchored 1536-B pieces
+    of 256-B rows, 16 lanes x 4 dword streams with A <- Z256(A) ^ w, the head row's clamp to the
+    16-B block holding the first byte (at absolute address base + S) and its realignment, the
+    Z4 Horner per lane, the quad and row trees, the Z1536 fold over pieces, Z4 and the tail bytes."""
+    E = S + slen
+    Ed, F4 = E & ~3, S & ~3
+    D, R, npc, h = rx_geometry(S, slen)
+    if npc == 0:
+        c = 0xFFFFFFFF
+        for b in buf[S:E]:
+            c = T1[(c ^ b) & 0xFF] ^ (c >> 8)
+        return c ^ 0xFFFFFFFF
+    pad = 64
+    mem = bytes(pad) + bytes(buf) + bytes(64)  # mem[pad + a] = buf[a]
+
+    def dw(a):
+        return struct.unpack_from("<I", mem, pad + a)[0]
+
+    lo = ((base + S) & ~15) - base  # buffer-relative clamp address
+    xl = (lo - F4) // 4
+    sa = S & 3
+    hm = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
+    C = 0
+    for p in range(npc):
+        pe = Ed - RX_PIECE * (npc - 1 - p)
+        A = [[0] * 4 for _ in range(16)]
+        u0 = RX_PR - h if p == 0 else 0
+        for u in range(u0, RX_PR):
+            for gl in range(16):
+                a = pe - RX_PIECE + 256 * u + 16 * gl
+                if p == 0:
+                    x = (a - F4) // 4
+                    al = max(a, lo)
+                    sh = min(max(xl - x, 0), 4)
+                    raw = [dw(al + 4 * j) for j in range(4)]
+                    v = [raw[j - sh] if j >= sh else 0 for j in range(4)]
+                    for j in range(4):
+                        xj = x + j
+                        d = v[j] if xj >= 0 else 0
+                        ci = 0
+                        if xj == 0:
+                            d &= hm
+                            ci = hm
+                        if xj == 1:
+                            ci = hm ^ 0xFFFFFFFF
+                        A[gl][j] = apply(Z256, A[gl][j]) ^ d ^ ci
+                else:
+                    for j in range(4):
+                        A[gl][j] = apply(Z256, A[gl][j]) ^ dw(a + 4 * j)
+        U = []
+        for gl in range(16):
+            t = apply(Z4, A[gl][0]) ^ A[gl][1]
+            t = apply(Z4, t) ^ A[gl][2]
+            U.append(apply(Z4, t) ^ A[gl][3])
+        quad = [Z48, Z32, Z16, None]
+        row = [Z192, Z128, Z64, None]
+        W = 0
+        for q in range(4):
+            qs = 0
+            for r in range(4):
+                u = U[4 * q + r]
+                qs ^= u if quad[r] is None else apply(quad[r], u)
+            W ^= qs if row[q] is None else apply(row[q], qs)
+        C = W if p == 0 else apply(Z1536, C) ^ W
+    reg = apply(Z4, C)
+    if npc > 1 and D - 384 * (npc - 1) == 1 and sa:
+        # frame dword 1 opens piece 1: its part of the CRC init, linear, added here
+        reg ^= zero_shift(apply(Z4, hm ^ 0xFFFFFFFF), 4 * D - 8)
+    for b in buf[Ed:E]:
+        reg = (reg >> 8) ^ T1[(reg ^ b) & 0xFF]
+    return reg ^ 0xFFFFFFFF

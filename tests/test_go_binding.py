@@ -3,8 +3,9 @@
 There is no Go toolchain in this image, so the files are checked for the surface they must
 provide, and tests/csrc/go_binding_replay.c replays DigestBatch / FillBatch / GPUs.DigestBatch
 exactly (4-byte aligned packing into fs_host_alloc pinned memory, 4 spare bytes per frame for
-the FCS, 16 spare bytes at the end) through the same C ABI calls; on the GPU its outputs must
-equal the oracle's bit for bit."""
+the FCS, 16 spare bytes at the end) through the same C ABI calls, and Group.DigestSharded (the
+RCCL group over every visible device, round-robin shards in device memory); on the GPU its
+outputs must equal the oracle's bit for bit."""
 import os
 import re
 import struct
@@ -31,7 +32,8 @@ def test_go_files_declare_the_binding():
     stacks = open(GO_STACKS).read()
     for sym in ("func OpenGPU(", "func (g *GPU) DigestBatch(", "func (g *GPU) FillBatch(", "func OpenGPUs(",
                 "func (m *GPUs) DigestBatch(", "C.fs_digest_batch_host(", "C.fs_fill_batch_host(",
-                "C.fs_digest_batch_multi(", "C.fs_host_alloc("):
+                "C.fs_digest_batch_multi(", "C.fs_host_alloc(", "func OpenGroup(", "func (g *Group) DigestSharded(",
+                "func ShardCount(", "C.fs_group_create(", "C.fs_digest_batch_sharded(", "C.fs_shard_count("):
         assert sym in eth, sym
     for sym in ("func (ps *PortStack) RecvEthBatch(", "func (ps *PortStack) recvEthVerified(", "deliverUDP", "deliverTCP"):
         assert sym in stacks, sym
@@ -80,7 +82,7 @@ def test_replay_built_and_loud_without_device(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,mtu", [("digest", 0), ("digest", 1514), ("multi", 0)])
+@pytest.mark.parametrize("mode,mtu", [("digest", 0), ("digest", 1514), ("multi", 0), ("sharded", 0), ("sharded", 1514)])
 def test_replay_digest_matches_oracle(tmp_path, mode, mtu):
     import framegen
 

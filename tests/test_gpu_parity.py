@@ -22,8 +22,8 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 @pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_WIDE, Engine.KERNEL_ALIGNED,
-                                        Engine.KERNEL_DUAL, Engine.KERNEL_AUTO],
-                ids=["one_pass", "mixed", "wide", "aligned", "dual", "auto"])
+                                        Engine.KERNEL_DUAL, Engine.KERNEL_AUTO, Engine.KERNEL_STREAM],
+                ids=["one_pass", "mixed", "wide", "aligned", "dual", "auto", "stream"])
 def engine(request):
     # every case through every kernel variant (and the automatic choice)
     if not torch.cuda.is_available():
@@ -358,5 +358,32 @@ def test_auto_choice_first_launches():
         assert kinds[:16] == [Engine.KERNEL_MIXED] * 16 and kinds[16:] == [Engine.KERNEL_ALIGNED] * 8, kinds
         check(e, buf, off, ln, label="uniform traffic after the window")
         assert e.last_kernel() == Engine.KERNEL_ALIGNED
+    finally:
+        e.close()
+
+
+def test_host_fill_after_failed_digest(monkeypatch):
+    """a host-staged digest that fails half-way (FS_FAULT_CHUNK injects FS_E_NOMEM
+    at chunk 1, after chunk 0's kernel and chunk 1's copy are queued on the copy streams) must not
+    leave copies in flight that corrupt the next host-staged call's staging: a TX fill right after
+    it is byte-exact against the oracle, and so is a digest on a fresh context."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from seqs_amd import FramesumError
+
+    monkeypatch.setenv("FS_FAULT_CHUNK", "1")
+    e = Engine(0)
+    monkeypatch.delenv("FS_FAULT_CHUNK")
+    try:
+        e.set_kernel(Engine.KERNEL_STREAM)
+        big, boff, bln = synth.uniform_batch(30000, 1500, seed=31)  # 45 MB: three 16-MiB chunks
+        with pytest.raises(FramesumError, match="injected"):
+            e.digest_host(big, boff.astype(np.uint64), bln.astype(np.uint32))
+        buf, off, ln = synth.mixed_batch(3000, seed=32)
+        exp = buf.copy()
+        edig, est = coracle.fill_batch(exp, off, ln, 0, 1)
+        got = buf.copy()
+        dig, st = e.fill_host(got, off, ln, 0, 1)
+        assert np.array_equal(got, exp) and np.array_equal(dig, edig) and np.array_equal(st, est)
     finally:
         e.close()
