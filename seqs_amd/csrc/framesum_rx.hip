@@ -61,6 +61,13 @@ static_assert(kWaveBytes % 16u == 0u && kSlotBytes % 16u == 0u, "16-B aligned he
 
 __shared__ __attribute__((aligned(16))) char g_lds[kLdsBytes];
 
+// section markers in the assembly (diagnostic builds only: -DFS_MARKS; tools/asm_sections.py)
+#ifdef FS_MARKS
+#define FS_MARK(name) asm volatile("; @@" name ::: "memory")
+#else
+#define FS_MARK(name) do { } while (0)
+#endif
+
 // the plain tables (FsTablesRx::plain_basis order, kRxPlain shifts)
 enum : uint32_t { kT4 = 0, kT16 = 1, kT32 = 2, kT48 = 3, kT64 = 4, kT128 = 5, kT192 = 6, kT1536 = 7 };
 
@@ -223,46 +230,53 @@ __device__ __forceinline__ void lean_row(const Keys& k, u32x4 v, uint32_t (&A)[4
     cs = sad16(v.w, cs);
 }
 
-// A head row. x: frame dword (relative to F4 = S & ~3) of the chunk's dword 0 as addressed; xl
-// (-3..0): the frame dword of the clamp address (the 16-B block that holds the frame's first byte;
-// chunks starting before it were loaded from there: realigned by sh dwords). Dwords before the
-// frame are zeroed, dword 0's bytes before S too; the CRC init XORs 0xFF into frame bytes [0, 4).
-// The chunks holding frame dwords [-xo, 28 - xo) are copied to the frame's header slot.
-__device__ __forceinline__ void head_row(const Keys& k, u32x4 u, int x, int xl, uint32_t sa, int xo, uint32_t slot,
-                                         uint32_t (&A)[4], uint32_t& cs) {
-    const int sh = min(max(xl - x, 0), 4);
-    uint32_t v[4];
-    v[0] = sh == 0 ? u.x : 0u;
-    v[1] = sh == 0 ? u.y : sh == 1 ? u.x : 0u;
-    v[2] = sh == 0 ? u.z : sh == 1 ? u.y : sh == 2 ? u.x : 0u;
-    v[3] = sh == 0 ? u.w : sh == 1 ? u.z : sh == 2 ? u.y : sh == 3 ? u.x : 0u;
-    const int c = x + xo;  // a multiple of 4
-    if (c >= 0 && c < kSlotDw) *reinterpret_cast<u32x4*>(g_lds + slot + 4u * (uint32_t)c) = u32x4{v[0], v[1], v[2], v[3]};
-    const uint32_t hm = 0xffffffffu << (8u * sa);
+// A head row (the rows that hold bytes before the frame or its first two dwords). x: frame dword
+// (relative to F4 = S & ~3) of the chunk's dword 0. Bytes before the frame are zeroed, and the CRC
+// init XORs 0xFF into frame bytes [0, 4): for dword j, t = the bytes of it before S (clamped to
+// 0..4); keep(t) = the bytes at or after S, and the init bytes are keep(t) & ~keep(t + 4).
+__device__ __forceinline__ uint32_t keep_mask(int t) {
+    const int c = min(max(t, 0), 4);
+    return (uint32_t)(0xffffffffull << (8 * c));
+}
+__device__ __forceinline__ void head_row(const Keys& k, const uint32_t (&v)[4], int x, uint32_t sa, uint32_t (&A)[4],
+                                         uint32_t& cs) {
+    const int b0 = (int)sa - 4 * x;  // chunk byte at which the frame starts
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int xj = x + j;
-        uint32_t d = xj >= 0 ? v[j] : 0u;
-        uint32_t ci = 0u;
-        if (xj == 0) { d &= hm; ci = hm; }
-        if (xj == 1) ci = ~hm;
-        A[j] = zrow(A[j], k, d ^ ci);
+        const uint32_t keep = keep_mask(b0 - 4 * j), init = keep & ~keep_mask(b0 - 4 * j + 4);
+        const uint32_t d = v[j] & keep;
+        A[j] = zrow(A[j], k, d ^ init);
         cs = sad16(d, cs);
     }
+}
+// The header slot: the chunks holding frame dwords [-xo, 28 - xo) (xo: frame dword 0's place in its
+// chunk) are copied to the frame's slot as they stream.
+__device__ __forceinline__ void capture(uint32_t slot, int x, int xo, const uint32_t (&v)[4]) {
+    const int c = x + xo;  // a multiple of 4
+    if (c >= 0 && c < kSlotDw) *reinterpret_cast<u32x4*>(g_lds + slot + 4u * (uint32_t)c) = u32x4{v[0], v[1], v[2], v[3]};
 }
 
 // ---------------------------------------------------------------------------------------
 // Frames of a tile. Lane L holds frame L & 15 of the tile (the 4 groups hold the same copy).
+// The head piece's geometry is derived here once per tile, so a step's assignment is a few
+// permutes and adds.
 struct Frames {
-    uint32_t slo, shi;  // frame offset
-    uint32_t slen;      // streamed length (kOpsFcs: without the FCS; 0 past the batch end)
-    uint32_t geo;       // pieces (bits 0..23; 0 = no rows) | head rows << 24
-    uint32_t tail;      // the dword at Ed (bytes [Ed, E) are the frame's tail; kOpsFcs: also FCS bytes)
-    uint32_t tail2;     // kOpsFcs: the dword after it
+    uint32_t slo, shi;    // frame offset
+    uint32_t slen;        // streamed length (kOpsFcs: without the FCS; 0 past the batch end)
+    uint32_t npc;         // pieces (0 = no rows: under 4 bytes past the first dword)
+    uint32_t pelo, pehi;  // absolute end of the head piece: frames + Ed - 1536 (npc - 1)
+    uint32_t meta;        // Dh (head piece dwords, 1..384) | dP << 9 | sa << 20
+    uint32_t tail;        // the dword at Ed (bytes [Ed, E) are the frame's tail; kOpsFcs: also FCS bytes)
+    uint32_t tail2;       // kOpsFcs: the dword after it
     __device__ __forceinline__ uint64_t S() const { return ((uint64_t)shi << 32) | slo; }
-    __device__ __forceinline__ uint32_t npc() const { return geo & 0xffffffu; }
-    __device__ __forceinline__ uint32_t h() const { return geo >> 24; }
 };
+// dP: where the head piece's grid (its 1536 B before pe) enters the memory page that holds the
+// frame's first byte, counted from the grid start (0: the grid lies in that page). Chunks before
+// dP load from the page start instead (realigned): reading before a frame never leaves the page of
+// its first byte. (Rows end at Ed, never past the frame.)
+__device__ __forceinline__ uint32_t meta_dh(uint32_t m) { return m & 511u; }
+__device__ __forceinline__ uint32_t meta_dp(uint32_t m) { return (m >> 9) & 2047u; }
+__device__ __forceinline__ uint32_t meta_sa(uint32_t m) { return (m >> 20) & 3u; }
 
 // Raw descriptors of a tile: plain loads, issued an assign call ahead of their use (a loop
 // iteration later, so hipcc cannot sink them; its counted wait lets the row ring run on).
@@ -283,12 +297,20 @@ __device__ __forceinline__ Frames derive(uint64_t S, uint32_t L, bool valid, con
     if (kOps == kOpsFcs) slen = slen >= 4u ? slen - 4u : 0u;
     f.slen = slen;
     const uint64_t E = S + slen, Ed = E & ~3ull, F4 = S & ~3ull;
-    f.geo = 0u;
+    f.npc = 0u;
+    f.meta = 0u;
+    const uint64_t base = reinterpret_cast<uint64_t>(frames);
     if (slen >= 4u && Ed >= S + 4u) {
         const uint32_t D = (uint32_t)((Ed - F4) >> 2);
-        const uint32_t R = (D + 63u) >> 6;
-        const uint32_t npc = (R + kPR - 1u) / kPR;
-        f.geo = npc | ((R - kPR * (npc - 1u)) << 24);
+        const uint32_t npc = (((D + 63u) >> 6) + kPR - 1u) / kPR;
+        const uint32_t Dh = D - 384u * (npc - 1u);
+        const uint64_t pe = base + Ed - (uint64_t)kPieceBytes * (npc - 1u);
+        const uint64_t page = (base + S) & ~4095ull, g0 = pe - kPieceBytes;
+        const uint32_t dP = page > g0 ? (uint32_t)(page - g0) : 0u;
+        f.npc = npc;
+        f.pelo = (uint32_t)pe;
+        f.pehi = (uint32_t)(pe >> 32);
+        f.meta = Dh | (dP << 9) | (((uint32_t)S & 3u) << 20);
     }
     // the tail dword and (FCS) the one after it: dword-aligned dwords that hold a byte of the
     // frame (or of its FCS), so they never leave the frame's memory pages
@@ -297,39 +319,49 @@ __device__ __forceinline__ Frames derive(uint64_t S, uint32_t L, bool valid, con
     f.tail2 = 0u;
     const uint32_t* tp = reinterpret_cast<const uint32_t*>(frames + Ed);
     const bool fcs = kOps == kOpsFcs && valid && L >= 4u;
-    if (f.geo != 0u && (t > 0u || fcs)) f.tail = tp[0];
-    if (f.geo != 0u && fcs && t > 0u) f.tail2 = tp[1];
+    if (f.npc != 0u && (t > 0u || fcs)) f.tail = tp[0];
+    if (f.npc != 0u && fcs && t > 0u) f.tail2 = tp[1];
     return f;
 }
 
 // ---------------------------------------------------------------------------------------
 // Steps.
 struct Step {
-    uint64_t base;  // address of this lane's chunk at position 0 (frames + piece end - 1536 + 16 gl)
-    uint64_t lo;    // clamp address: the 16-B block holding the frame's first byte
+    uint64_t base;  // address of this lane's chunk at position 0 (piece end - 1536 + 16 gl)
     int rel0;       // frame dword (relative to F4) of that chunk's dword 0
-    uint32_t info;  // frame (0..3) | active << 4 | sa << 5 | xo << 7 | (-xl) << 9 | piece 1 << 11
+    uint32_t info;  // frame (0..15) | active << 4 | sa << 5 | xo << 7 | dP << 9
     __device__ __forceinline__ uint32_t f() const { return info & 15u; }
     __device__ __forceinline__ bool active() const { return (info >> 4) & 1u; }
     __device__ __forceinline__ uint32_t sa() const { return (info >> 5) & 3u; }
     __device__ __forceinline__ int xo() const { return (int)((info >> 7) & 3u); }
-    __device__ __forceinline__ int xl() const { return -(int)((info >> 9) & 3u); }
+    __device__ __forceinline__ uint32_t dP() const { return info >> 9; }
 };
 // wave-uniform step parameters
 struct StepU {
     int kind;         // 1 head pieces, 0 other pieces, -1 none (the wave is done)
     int start;        // first consumed position
-    int clamp_until;  // loads at positions <= this are clamped to Step::lo
     int mask_until;   // positions <= this take the head-row path
-    int cap0;         // round 1: position 0 may hold header chunks
+    int cap_until;    // positions <= this may hold header-slot chunks
+    int clamp_until;  // rare: loads at positions <= this are clamped into the frame's page (realigned)
     int last;         // the last step of its tile: the tile is finished after it
 };
 
 // The row loads of one step (unconditional: one load per position, so the ring's wait counts are static).
-__device__ __forceinline__ u32x4 load_pos(const Step& s, const StepU& su, int u) {
+__device__ __forceinline__ u32x4 load_pos(const Step& s, const StepU& su, int u, uint32_t gl) {
     uint64_t a = s.base + 256u * (uint32_t)u;
-    if (u <= su.clamp_until) a = a < s.lo ? s.lo : a;
+    if (u <= su.clamp_until) {  // rare: the head grid starts in the page before the frame's first byte
+        const uint64_t lo = s.base - 16u * gl + s.dP();
+        a = a < lo ? lo : a;
+    }
     return *reinterpret_cast<gu32x4*>(a);
+}
+// A clamped chunk realigned to where it belongs (rare path): sh dwords of shift, zeros before.
+__device__ __forceinline__ void realign(uint32_t (&v)[4], int sh) {
+    const uint32_t u0 = v[0], u1 = v[1], u2 = v[2], u3 = v[3];
+    v[0] = sh == 0 ? u0 : 0u;
+    v[1] = sh == 0 ? u1 : sh == 1 ? u0 : 0u;
+    v[2] = sh == 0 ? u2 : sh == 1 ? u1 : sh == 2 ? u0 : 0u;
+    v[3] = sh == 0 ? u3 : sh == 1 ? u2 : sh == 2 ? u1 : sh == 3 ? u0 : 0u;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -455,13 +487,24 @@ __device__ __forceinline__ Parsed parse_frame(const Slot& V, uint32_t len, uint3
 #pragma unroll
     for (int i = 0; i < 6; ++i) t += (int64_t)(odd ? w[i] : bswap16(w[i]));
     r.corr_fixed = t;
-    // the Ethernet + IP header bytes [0, off) (off <= 74: frame dwords < 20, all in the slot)
+    // the Ethernet + IP header bytes [0, off): big-endian words (off = 4q + 2: frame dwords 0 .. q-1
+    // and the high half of dword q), moved into the 16-bit-half domain as the words above
     {
-        const int a1 = (int)(V.sa + off);
         uint32_t s = 0;
 #pragma unroll
-        for (int x = 0; x < 20; ++x) s = sad16(V.dw(x) & range_mask(x, (int)V.sa, a1), s);
-        t -= (int64_t)s;
+        for (int j = 0; j < 3; ++j) {
+            const uint32_t d = __builtin_bswap32(V.fdw(j));
+            s += (d >> 16) + (d & 0xffffu);
+        }
+#pragma unroll
+        for (int j = 3; j < 9; ++j) s += j < q ? (bs[j] >> 16) + (bs[j] & 0xffffu) : 0u;
+        for (int j = 9; j < q; ++j) {  // IP options past dword 8 (rare)
+            const uint32_t d = __builtin_bswap32(V.fdw(j));
+            s += (d >> 16) + (d & 0xffffu);
+        }
+        s += lb[0] >> 16;
+        s = fold16(fold16(s));
+        t -= (int64_t)(odd ? s : bswap16(s));
     }
     if (end < len) {  // Ethernet padding [end, len)
         const int a0 = (int)(V.sa + end), a1 = (int)(V.sa + len);
@@ -488,8 +531,10 @@ __device__ __forceinline__ uint32_t finish_l4(const Parsed& P, uint32_t main_sum
     int64_t t = P.direct ? (int64_t)P.l4sum + P.corr_fixed : (int64_t)main_sum + P.corr;
     t += 65535LL * (1LL << 20);
     uint64_t x = (uint64_t)t;
-    x = (x & 0xffffffffu) + (x >> 32);
-    while (x >> 16) x = (x & 0xffffu) + (x >> 16);
+    x = (x & 0xffffffffu) + (x >> 32);  // < 2^33
+    x = (x & 0xffffu) + (x >> 16);      // < 2^18
+    x = (x & 0xffffu) + (x >> 16);      // < 2^16 + 4
+    x = (x & 0xffffu) + (x >> 16);      // <= 0xFFFF
     uint32_t l4 = (~(uint32_t)x) & 0xffffu;
     if (!P.parity) l4 = bswap16(l4);
     verdict = (l4 == P.stored) ? V_OK : V_CSUM;
@@ -543,18 +588,17 @@ __device__ __forceinline__ void finish_frame(const Frames& F, uint32_t fi, uint3
     const uint64_t E = S + slen, Ed = E & ~3ull, F4 = S & ~3ull;
     const uint32_t t = (uint32_t)(E - Ed);
     const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + F4);
-    if (F.npc() == 0u) {
+    if (F.npc == 0u) {
         finish_tiny<kOps>(F, fi, frames, wframes, lengths, out, status, tx);
         return;
     }
     uint32_t crcv, fcs = 0u, cs = 0u;
     Parsed P;
     {
-        const uint32_t npc = F.npc();
-        const uint64_t pe0 = Ed - (uint64_t)kPieceBytes * (npc - 1u);  // the head piece's end
+        const uint32_t npc = F.npc;
         Slot V;
         V.sb = wb + i * kSlotBytes;
-        V.xo = (int)(((F4 - pe0) >> 2) & 3u);
+        V.xo = (int)((0u - meta_dh(F.meta)) & 3u);
         V.D = (int)((Ed - F4) >> 2);
         V.tail = F.tail;
         V.sa = sa;
@@ -609,8 +653,9 @@ __device__ __forceinline__ void finish_frame(const Frames& F, uint32_t fi, uint3
 // The kernel.
 //
 // Per wave: an assigner that runs one step ahead of the consumer. The assigner walks its tile's
-// head steps then its rounds, and moves to the wave's next tile (T1) when they are exhausted; the
-// consumer finishes its tile (T0) after that tile's last step and takes T1 over.
+// head steps then its rounds, reading the tile's frames from T1; when they are exhausted it moves
+// T1 on to the wave's next tile. The consumer finishes its tile (T0, a copy of T1 taken when the
+// consumer reached that tile) after the tile's last step.
 template <uint32_t kOps>
 __global__ void __launch_bounds__(kThreads, 4)
 rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
@@ -642,37 +687,46 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
     uint32_t a_next = gwave;         // the tile whose raw descriptors are in (rS, rL)
     int a_done = 0, a_pend = 0;      // a_pend: its tile's last step is out, advance at the next call
     int a_phase = 0, a_k = 0, a_p = 0, a_nh = 0, a_cnt = 0, a_maxnpc = 0;
-    Frames T0, T1;                   // the consumer's tile, the assigner's next tile
+    Frames T0, T1;                   // the consumer's tile, the assigner's tile
     uint32_t c_tile = 0;             // the consumer's tile index
 
-    // Switch the assigner to the wave's next tile that has steps; tiles whose frames are all under
-    // the stream minimum are finished right here. Returns false when the wave has no tile left.
-    // Called one assign call after the previous tile's last step was produced: by then the consumer
-    // has taken T1 over (a tile of one step is consumed right after the step before it).
-    // the head order of the assigner's new tile T1 (frames with rows, by head rows, descending,
-    // then index) into the wave's order bytes; returns the frames with rows
+    // The head order of T1's tile (frames with rows, by head rows descending, then index) into the
+    // wave's order bytes; returns the number of frames with rows.
     auto schedule = [&]() __attribute__((always_inline)) -> int {
-        const uint32_t npc = T1.npc(), h = T1.h();
+        const uint32_t npc = T1.npc, dh = meta_dh(T1.meta);
+        const uint32_t h = (dh + 63u) >> 6;
         const uint32_t mR = (uint32_t)__ballot(npc > 0u) & 0xffffu;
-        uint32_t rank = 0, maxnpc = 0;
-        for (uint32_t m = mR; m; m &= m - 1u) {
-            const uint32_t j = __builtin_ctz(m);
-            const uint32_t hj = __builtin_amdgcn_readlane(h, j), nj = __builtin_amdgcn_readlane(npc, j);
-            rank += (hj > h || (hj == h && j < gl)) ? 1u : 0u;
-            maxnpc = nj > maxnpc ? nj : maxnpc;
+        a_nh = __builtin_popcount(mR);
+        // the pieces of the longest frame: a max over the row of 16 frames
+        uint32_t m = npc;
+        m = max(m, dpp<0x121>(m));
+        m = max(m, dpp<0x122>(m));
+        m = max(m, dpp<0x124>(m));
+        m = max(m, dpp<0x128>(m));
+        a_maxnpc = (int)__builtin_amdgcn_readfirstlane(m);
+        uint32_t rank;
+        const uint32_t h0 = mR ? __builtin_amdgcn_readlane(h, __builtin_ctz(mR)) : 0u;
+        if (((uint32_t)__ballot(npc > 0u && h == h0) & 0xffffu) == mR) {
+            rank = __builtin_amdgcn_mbcnt_lo(mR, 0u);  // one head length (a uniform batch): index order
+        } else {
+            rank = 0u;
+            for (uint32_t mm = mR; mm; mm &= mm - 1u) {
+                const uint32_t j = __builtin_ctz(mm);
+                const uint32_t hj = __builtin_amdgcn_readlane(h, j);
+                rank += (hj > h || (hj == h && j < gl)) ? 1u : 0u;
+            }
         }
-        a_maxnpc = (int)maxnpc;
         if (lane < 16u && npc > 0u) g_lds[wb + kWO + rank] = (char)lane;
         a_phase = 0;
         a_k = 0;
-        a_nh = __builtin_popcount(mR);
         return a_nh;
     };
-    // Switch the assigner to the wave's next tile that has steps (T1); tiles whose frames are all
+    // Move the assigner to the wave's next tile that has steps (into T1); tiles whose frames are all
     // under the stream minimum are finished right here. Returns false when the wave has no tile
     // left. Called one assign call after the previous tile's last step was produced: by then the
-    // consumer has taken T1 over (a tile of one step is consumed right after the step before it).
+    // consumer has copied T1 (a tile of one step is consumed right after the step before it).
     auto advance = [&]() __attribute__((always_inline)) -> bool {
+        FS_MARK("advance");
         if (a_next >= ntiles) return false;
         a_tile = a_next;
         T1 = derive<kOps>(rS, rL, a_tile * 16u + gl < n, frames);  // (rS, rL): loaded a block ago
@@ -706,19 +760,18 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
             su.last = 0;
             return;
         }
-        // the assigner's frames: T1 while the consumer still holds an earlier tile
-        const bool in1 = a_tile != c_tile;
-        const Frames& A = in1 ? T1 : T0;
-        int k = a_k, p = 0, count;
+        FS_MARK("produce");
+        const int k = a_k;
+        int p = 0, count;
         if (a_phase == 0) {
             count = a_nh;
         } else {
             p = a_p;
             if (a_k == 0) {  // a round starts: the frames with a piece p, in index order
-                const uint32_t mP = (uint32_t)__ballot(A.npc() > (uint32_t)p) & 0xffffu;
+                const uint32_t mP = (uint32_t)__ballot(T1.npc > (uint32_t)p) & 0xffffu;
                 a_cnt = __builtin_popcount(mP);
                 const uint32_t pos = __builtin_amdgcn_mbcnt_lo(mP, 0u);
-                if (lane < 16u && A.npc() > (uint32_t)p) g_lds[wb + kWO + pos] = (char)lane;
+                if (lane < 16u && T1.npc > (uint32_t)p) g_lds[wb + kWO + pos] = (char)lane;
             }
             count = a_cnt;
         }
@@ -726,53 +779,62 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
         const bool act = sidx < count;
         const uint32_t f = (uint32_t)(uint8_t)g_lds[wb + kWO + (act ? sidx : 4 * k)];
         const int src = (int)((grp * 16u + f) << 2);
-        const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)A.slo);
-        const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)A.shi);
-        const uint32_t slen = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)A.slen);
-        const uint32_t geo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)A.geo);
-        const uint64_t S = ((uint64_t)shi << 32) | slo;
-        const uint64_t E = S + slen, Ed = E & ~3ull, F4 = S & ~3ull;
-        const uint32_t npc = geo & 0xffffffu, h = geo >> 24;
-        const uint64_t pe = Ed - (uint64_t)kPieceBytes * (npc - 1u - (uint32_t)p);
-        const uint64_t g0 = pe - kPieceBytes + 16u * gl;
-        s.base = reinterpret_cast<uint64_t>(frames) + g0;
-        s.lo = (reinterpret_cast<uint64_t>(frames) + S) & ~15ull;
-        s.rel0 = (int)((int64_t)(g0 - F4) >> 2);
-        const uint32_t xo = (uint32_t)((F4 - pe) >> 2) & 3u;
-        const uint32_t nxl = (uint32_t)((reinterpret_cast<uint64_t>(frames) + F4 - s.lo) >> 2) & 3u;
-        s.info = f | (act ? 16u : 0u) | (((uint32_t)S & 3u) << 5) | (xo << 7) | (nxl << 9);
+        const uint32_t pelo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)T1.pelo);
+        const uint32_t pehi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)T1.pehi);
+        const uint32_t meta = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)T1.meta);
+        const uint32_t dh = meta_dh(meta), sa = meta_sa(meta);
+        // chunk at position 0: piece end (head + 1536 p) - 1536 + 16 gl
+        const int off0 = 1536 * (p - 1) + 16 * (int)gl;
+        s.base = (((uint64_t)pehi << 32) | pelo) + (uint64_t)(int64_t)off0;
+        s.rel0 = (int)dh - 384 + 384 * p + 4 * (int)gl;
+        s.info = f | (act ? 16u : 0u) | (sa << 5) | (((0u - dh) & 3u) << 7) | (p == 0 ? (meta_dp(meta) << 9) : 0u);
         int last;
+        su.start = 0;
+        su.mask_until = -1;
+        su.cap_until = -1;
+        su.clamp_until = -1;
         if (a_phase == 0) {
-            const int hmax = (int)__builtin_amdgcn_readlane(h, 0);
+            // per group: its head rows, the row of frame dword 1 (0: S is dword aligned; the
+            // init and the masks end there), the row of the last header-slot dword, the clamp
             const int glast = min(3, a_nh - 1 - 4 * k);
-            const int hmin = (int)__builtin_amdgcn_readlane(h, 16 * glast);
+            int hmax = 0, mrow = -1, crow = -1, clamp = -1;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                if (g > glast) break;
+                const uint32_t mg = __builtin_amdgcn_readlane(meta, 16 * g);
+                const int dg = (int)meta_dh(mg);
+                const int xm = meta_sa(mg) ? 1 : 0;
+                const int xo = (int)((0u - (uint32_t)dg) & 3u);
+                hmax = max(hmax, (dg + 63) >> 6);
+                mrow = max(mrow, (xm + 384 - dg) >> 6);
+                crow = max(crow, (kSlotDw - 1 - xo + 384 - dg) >> 6);
+                const int dp = (int)meta_dp(mg);
+                if (dp > 0) clamp = max(clamp, (dp - 1) >> 8);
+            }
             su.kind = 1;
             su.start = kPR - hmax;
-            su.clamp_until = kPR - hmin;
-            su.mask_until = min(kPR - 1, kPR - hmin + 1);
-            su.cap0 = 0;
-            ++k;
-            if (4 * k >= a_nh) {  // the head steps are done
+            su.mask_until = min(kPR - 1, mrow);
+            su.cap_until = min(kPR - 1, crow);
+            su.clamp_until = clamp;
+            ++a_k;
+            if (4 * a_k >= a_nh) {  // the head steps are done
                 a_phase = 1;
                 a_p = 1;
-                k = 0;
+                a_k = 0;
             }
             last = (a_phase == 1 && a_maxnpc <= 1) ? 1 : 0;
         } else {
             su.kind = 0;
-            su.start = 0;
-            su.clamp_until = -1;
-            su.mask_until = -1;
-            su.cap0 = p == 1 ? 1 : 0;
-            ++k;
+            // round 1: header-slot chunks past a short head piece (in piece 1's first row)
+            su.cap_until = p == 1 ? 0 : -1;
+            ++a_k;
             last = 0;
-            if (4 * k >= a_cnt) {
-                k = 0;
+            if (4 * a_k >= a_cnt) {
+                a_k = 0;
                 ++a_p;
                 if (a_p >= a_maxnpc) last = 1;
             }
         }
-        a_k = k;
         su.last = last;
         a_pend = last;
     };
@@ -793,7 +855,7 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
         assign(nxt, nu, z, zu);
     }
 #pragma unroll
-    for (int u = 0; u < kPR; ++u) ring[u] = load_pos(nxt, nu, u);
+    for (int u = 0; u < kPR; ++u) ring[u] = load_pos(nxt, nu, u, gl);
     cur = nxt;
     cu = nu;
     assign(nxt, nu, cur, cu);
@@ -805,19 +867,27 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
 #pragma unroll
         for (int u = 0; u < kPR; ++u) {
             if (u >= cu.start) {
+                uint32_t v[4] = {ring[u].x, ring[u].y, ring[u].z, ring[u].w};
+                const int x = cur.rel0 + 64 * u;
+                if (u <= cu.clamp_until) {  // rare: chunks loaded from the frame's page start
+                    FS_MARK("realign");
+                    realign(v, min(max(((int)cur.dP() - 256 * u - 16 * (int)gl) >> 2, 0), 4));
+                }
+                if (u <= cu.cap_until) capture(slot, x, cur.xo(), v);
                 if (u <= cu.mask_until) {
-                    head_row(keys, ring[u], cur.rel0 + 64 * u, cur.xl(), cur.sa(), cur.xo(), slot, A, cs);
+                    FS_MARK("head_row");
+                    head_row(keys, v, x, cur.sa(), A, cs);
                 } else {
-                    if (u == 0 && cu.cap0) {  // round 1: header chunks past a one-row head piece
-                        const int c = cur.rel0 + cur.xo();
-                        if (c >= 0 && c < kSlotDw) *reinterpret_cast<u32x4*>(g_lds + slot + 4u * (uint32_t)c) = ring[0];
-                    }
+                    FS_MARK("lean_row");
                     lean_row(keys, ring[u], A, cs);
                 }
             }
-            ring[u] = load_pos(nxt, nu, u);
+            FS_MARK("load");
+            ring[u] = load_pos(nxt, nu, u, gl);
+            FS_MARK("pos_end");
         }
         // ---- combine the group's piece: W (its pending CRC register) and its sum
+        FS_MARK("combine");
         {
             const uint32_t c4 = pcst(kT4);
             uint32_t U = zt(A[0], c4) ^ A[1];
@@ -847,17 +917,21 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
                 }
             }
         }
+        FS_MARK("after_combine");
         if (cu.last) {
+            FS_MARK("finish");
             // ---- the consumer's tile is complete: parse and finish its frames
             if (lane < 16u && c_tile * 16u + lane < n)
                 finish_frame<kOps>(T0, c_tile * 16u + lane, wb, lane, mtu, frames, wframes, lengths, out, status, tx);
             T0 = T1;
             c_tile = a_tile;
         }
+        FS_MARK("assign");
         cur = nxt;
         cu = nu;
         assign(nxt, nu, cur, cu);
         load_raw(min(a_next, ntiles - 1u), gl, n, offsets, lengths, rS, rL);
+        FS_MARK("loop_end");
     }
 }
 

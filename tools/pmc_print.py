@@ -14,7 +14,7 @@ for cfgdir in sorted({os.path.basename(p).split("_")[0] for p in glob.glob(os.pa
     for path in glob.glob(os.path.join(root, cfgdir + "_*", "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "digest_kernel" in row["Kernel_Name"]:
+                if "digest_kernel" in row["Kernel_Name"] or "rx_kernel" in row["Kernel_Name"]:
                     per[(row["Counter_Name"], path, row["Dispatch_Id"])] += float(row["Counter_Value"])
     by = defaultdict(list)
     for (name, _, _), v in per.items():
