@@ -13,10 +13,12 @@ batches (> 256 MiB in total) are rotated so the 256 MiB Infinity Cache cannot
 serve them. Multi-GPU (torchrun, one process per GPU, RCCL = torch "nccl"):
 every rank digests its own shard (weak scaling, frame i of the global batch
 on rank i mod N) and the per-frame digests + verdicts are gathered to rank 0
-over RCCL, one gather per group of --gather-every steps, overlapped with the next
-group's kernels; no other collective. Rank 0 receives the shards as they are (global
-frame j*N + r is local frame j of rank r: seqs_amd.shard.gather_digests shows the
-interleave; the bench does not spend a rank-0 kernel on it).
+over RCCL, one gather per group of steps (gather_plan: about half of each stream's steps
+in the region, at most --gather-every), overlapped with the next group's kernels; no other
+collective. Rank 0 receives the shards as they are (global frame j*N + r is local frame j
+of rank r: seqs_amd.shard.gather_digests shows the interleave; the bench does not spend a
+rank-0 kernel on it). With N > 1 the same line also carries "c4_strong": the C4 strong-scaled
+measurement (BASELINE configs[3], the config the >= 3.5x-at-4-GPUs target is quoted on).
 
 Prints ONE JSON line on rank 0 (see the contract in DESIGN.md §5).
 """
@@ -57,8 +59,10 @@ def parse():
                         "affinity mask); the 1-thread figure is measured beside it")
     p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather (N>1 diagnostics)")
     p.add_argument("--gather-every", type=int, default=64,
-                   help="N>1: each stream sends the digests + verdicts of this many of its steps to rank 0 in "
-                        "one RCCL gather (one collective per group, not two per step)")
+                   help="N>1: at most this many of a stream's steps per RCCL gather of digests + verdicts to rank "
+                        "0 (gather_plan: about half of each stream's steps in the region, so the region does not "
+                        "end in one drain of all its slabs)")
+    p.add_argument("--no-c4", action="store_true", help="N>1: skip the C4 strong-scaled record in the line")
     p.add_argument("--force-gather", action="store_true",
                    help="run the gather path on a single GPU too (a 1-rank process group; a test of the N>1 loop)")
     p.add_argument("--op", choices=["digest", "fill", "fcs"], default="digest",
@@ -106,6 +110,33 @@ def with_room(buf, off, ln, room: int = 4):
     for o, no, l in zip(off, noff, ln):
         nbuf[no : no + l] = buf[o : o + l]
     return nbuf, noff, ln
+
+
+def gather_plan(steps: int, streams: int, every: int) -> int:
+    """Steps per gather group for a region of `steps` steps over `streams` streams: each stream
+    runs q = ceil(steps / streams) of them; a group holds about half of them (at most `every`),
+    so every stream's first group goes to rank 0 while its second is still being digested and
+    the region ends with at most half of its slabs in flight."""
+    q = (max(1, steps) + max(1, streams) - 1) // max(1, streams)
+    return max(1, min(max(1, every), (q + 1) // 2))
+
+
+def gather_schedule(steps: int, streams: int, G: int):
+    """The gathers one region issues, in issue order: (after_step, stream, group, slabs) for every
+    full group (issued right after its last step) and then, at the drain, every stream's partly
+    filled group. Slots of stream s: group g, slab j holds the region's step s + streams*(2*G*k + G*g + j)
+    for some k. (The step loop below follows exactly this schedule; tests/test_bench_plan.py checks it.)"""
+    out = []
+    for i in range(steps):
+        si, q = i % streams, i // streams
+        g, j = (q // G) % 2, q % G
+        if j == G - 1:
+            out.append((i, si, g, G))
+    for si in range(streams):
+        q_end = (steps - si + streams - 1) // streams if steps > si else 0
+        if q_end % G:
+            out.append((steps, si, (q_end // G) % 2, q_end % G))
+    return out
 
 
 def cpu_model() -> str:
@@ -231,7 +262,7 @@ def main():
     # With the gather, each stream owns 2 groups of G slots for its own consecutive steps; when
     # a group is full, that stream hands its slabs to rank 0 in one RCCL gather (issued on that
     # stream, so it waits for that stream's kernels only) while it fills the other group.
-    G = max(1, args.gather_every) if gather else 1
+    G = gather_plan(args.steps, ns, args.gather_every) if gather else 1
     nslot = max(2, ns)
     slab = (9 * n + 255) // 256 * 256
 
@@ -249,18 +280,20 @@ def main():
         stage = torch.empty(ns * G * slab, dtype=torch.uint8, device=dev)
         recv_stage = [torch.empty_like(stage) for _ in range(world)] if rank == 0 else None
         pend = [[None, None] for _ in range(ns)]  # per stream and group: the RCCL work of its latest gather
+        issued = []  # (after_step, stream, group, slabs) of the region's gathers (== gather_schedule)
         last = {}  # (stream, group) -> ("own" | "all", slabs): which gather delivered it last
     flat = torch.empty(nslot * slab, dtype=torch.uint8, device=dev)
     outs, stats = zip(*[views(flat, k) for k in range(nslot)])
 
-    def step(i: int):
+    def step(i: int, r: int):
+        """step i overall, r-th step of its region (the gather groups restart with each region)"""
         fb, fo, fl = batches[i % nb]
-        si = i % ns
+        si = r % ns
         s = streams[si]
         if not gather:
             run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=s)
             return
-        q = i // ns
+        q = r // ns
         g, j = (q // G) % 2, q % G
         with torch.cuda.stream(s):
             if j == 0 and pend[si][g] is not None:
@@ -271,14 +304,15 @@ def main():
             if j == G - 1:
                 pend[si][g] = dist.gather(gbuf[si][g], recv[si][g], dst=0, async_op=True)
                 last[(si, g)] = ("own", G)
+                issued.append((r, si, g, G))
 
-    def drain(i_end: int):
+    def drain(r_end: int):
         if not gather:
             return
-        # partly filled groups still go to rank 0 (same calls on every rank: i_end is common)
+        # partly filled groups still go to rank 0 (same calls on every rank: r_end is common)
         part = []
         for si in range(ns):
-            q_end = (i_end - si + ns - 1) // ns  # steps this stream ran
+            q_end = (r_end - si + ns - 1) // ns if r_end > si else 0  # steps this stream ran
             g = (q_end // G) % 2
             if q_end % G != 0 and pend[si][g] is None:
                 part.append((si, g, q_end % G))  # (stream, group, slabs written in it)
@@ -296,12 +330,14 @@ def main():
             for si in range(ns):
                 pend[si][g] = work
                 last[(si, g)] = ("all", m)
+            issued.extend((r_end, si, g, k) for si, g, k in part)
         else:
             for si, g, k in part:
                 with torch.cuda.stream(streams[si]):
                     rv = [r[: k * slab] for r in recv[si][g]] if rank == 0 else None
                     pend[si][g] = dist.gather(gbuf[si][g][: k * slab], rv, dst=0, async_op=True)
                 last[(si, g)] = ("own", k)
+                issued.append((r_end, si, g, k))
         for si in range(ns):
             for g in range(2):
                 if pend[si][g] is not None:
@@ -318,9 +354,12 @@ def main():
         run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=streams[i % ns])
     torch.cuda.synchronize()
     for i in range(args.warmup):
-        step(i)
+        step(i, i)
     drain(args.warmup)
     torch.cuda.synchronize()
+    if gather:
+        last.clear()  # the checks below cover the timed region's gathers
+        issued.clear()
 
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks
     if world > 1:
@@ -328,8 +367,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
-    drain(args.warmup + args.steps)
+        step(args.warmup + i, i)
+    drain(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -339,6 +378,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if gather:
+        assert issued == gather_schedule(args.steps, ns, G), "the region's gathers differ from gather_schedule"
     if gather and rank == 0:
         # every group's latest gather delivered rank 0's own slabs intact (a check of the loop)
         torch.cuda.synchronize()
@@ -423,8 +464,19 @@ def main():
             },
             "cpu_baseline": cpu,
         }
-        print(json.dumps(result), flush=True)
     engine.close()
+    del batches, flat
+    if gather:
+        del gbuf, recv, stage, recv_stage
+    if world > 1 and args.config == "c2" and args.op == "digest" and not args.no_c4:
+        # the C4 strong-scaled record beside the weak-scaled C2 value (same steps / warmup)
+        torch.cuda.empty_cache()
+        c4 = run_c4(args, world, rank, local, dev, frames=1 << 20)
+        if rank == 0:
+            result["c4_strong"] = {k: c4[k] for k in ("value", "unit", "ms_per_step", "scaling", "config")}
+            result["c4_strong"]["kernel_avg_us"] = c4["roofline"]["kernel_avg_us"]
+    if rank == 0:
+        print(json.dumps(result), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
     return result
@@ -449,6 +501,23 @@ def time_region(world, dist, torch, body):
 
 
 def main_c4(args, world, rank, local, dev):
+    result = run_c4(args, world, rank, local, dev, frames=args.frames or (1 << 20))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist_initialized():
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    return result
+
+
+def dist_initialized() -> bool:
+    import torch.distributed as dist
+
+    return dist.is_available() and dist.is_initialized()
+
+
+def run_c4(args, world, rank, local, dev, frames):
     """C4 (BASELINE configs[3]): one global batch of 1,048,576 x 1500-B frames per step,
     frame i on rank i mod N (strong scaling). A step: every rank digests its shard into a
     slab (digests + verdicts, fs_shard_slab_bytes layout), RCCL gathers the slabs to rank 0,
@@ -459,7 +528,7 @@ def main_c4(args, world, rank, local, dev):
 
     from seqs_amd import Engine, shard_count, shard_slab_bytes
 
-    n_global = args.frames or (1 << 20)
+    n_global = frames
     engine = Engine(local)
     n = shard_count(n_global, world, rank)
     m = (n_global + world - 1) // world
@@ -596,10 +665,10 @@ def main_c4(args, world, rank, local, dev):
             "cpu_baseline": cpu_baseline("c4", args.cpu_seconds, args.cpu_threads)
             if world == 1 and args.cpu_seconds > 0 else None,
         }
-        print(json.dumps(result), flush=True)
+    else:
+        result = None
     engine.close()
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    return result
 
 
 def main_c5(args):

@@ -3,7 +3,9 @@
 // gfx950 kernel (through fs_digest_batch on its own context and stream); RCCL (ncclGather over
 // xGMI) brings the 8-byte digests and 1-byte verdicts to the first device, where the
 // de-interleave kernel (framesum_shard.hip) restores global frame order. Frames are
-// independent (eth/crc.go:12-17), so the gather is the only collective.
+// independent (eth/crc.go:12-17), so the gather is the only collective. The batch goes in
+// chunks (framesum_plan.h chunk_rows): chunk c's transfer and de-interleave run on a second
+// stream per device while the devices digest chunk c+1.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -21,6 +23,8 @@ struct fs_group {
     std::vector<fs_ctx*> ctx;
     std::vector<ncclComm_t> comm;
     std::vector<hipStream_t> stream;
+    std::vector<hipStream_t> xfer;  // per device: the gather (and on the first device the de-interleave)
+    std::vector<hipEvent_t> done;   // per device and chunk: that chunk's shard kernel has finished
     std::vector<uint8_t*> send;  // per device k >= 1: its slab; device 0 sends in place from recv
     uint8_t* recv = nullptr;     // first device: n slabs back to back
     uint64_t cap_slab = 0;       // bytes per slab currently allocated
@@ -30,6 +34,11 @@ struct fs_group {
 namespace {
 
 thread_local std::string g_group_create_err;
+
+// chunks per call: about 32K rows each (a digest launch of ~50 MB of 1500-B frames, long enough to
+// run at full rate), at most kMaxChunks
+constexpr uint32_t kMaxChunks = 8;
+constexpr uint64_t kChunkRows = 32768;
 
 fs_status gset(fs_group* g, fs_status code, const std::string& msg) {
     if (g) g->err = msg;
@@ -58,6 +67,7 @@ fs_status ensure_slabs(fs_group* g, uint64_t sb) {
     for (int k = 0; k < g->n; ++k) {
         (void)hipSetDevice(g->dev[k]);
         (void)hipStreamSynchronize(g->stream[k]);
+        (void)hipStreamSynchronize(g->xfer[k]);
     }
     free_slabs(g);
     if (hipSetDevice(g->dev[0]) != hipSuccess || hipMalloc(&g->recv, sb * (uint64_t)g->n) != hipSuccess)
@@ -97,6 +107,8 @@ fs_status fs_group_create(const int* devices, int ndev, fs_group** out) {
         g->ctx.assign(ndev, nullptr);
         g->comm.assign(ndev, nullptr);
         g->stream.assign(ndev, nullptr);
+        g->xfer.assign(ndev, nullptr);
+        g->done.assign((size_t)ndev * kMaxChunks, nullptr);
         g->send.assign(ndev, nullptr);
     } catch (const std::bad_alloc&) {
         delete g;
@@ -111,6 +123,9 @@ fs_status fs_group_create(const int* devices, int ndev, fs_group** out) {
         }
         hipError_t e = hipSetDevice(devices[k]);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->stream[k], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->xfer[k], hipStreamNonBlocking);
+        for (uint32_t c = 0; c < kMaxChunks && e == hipSuccess; ++c)
+            e = hipEventCreateWithFlags(&g->done[(size_t)k * kMaxChunks + c], hipEventDisableTiming);
         if (e != hipSuccess) {
             const std::string msg = std::string("fs_group_create: stream: ") + hipGetErrorString(e);
             fs_group_destroy(g);
@@ -131,18 +146,18 @@ fs_status fs_group_create(const int* devices, int ndev, fs_group** out) {
 fs_status fs_group_destroy(fs_group* g) {
     if (!g) return FS_E_INVALID;
     for (int k = 0; k < g->n; ++k) {
-        if (g->stream[k]) {
-            (void)hipSetDevice(g->dev[k]);
-            (void)hipStreamSynchronize(g->stream[k]);
-        }
+        (void)hipSetDevice(g->dev[k]);
+        if (g->stream[k]) (void)hipStreamSynchronize(g->stream[k]);
+        if (g->xfer[k]) (void)hipStreamSynchronize(g->xfer[k]);
     }
     free_slabs(g);
     for (int k = 0; k < g->n; ++k) {
         if (g->comm[k]) (void)ncclCommDestroy(g->comm[k]);
-        if (g->stream[k]) {
-            (void)hipSetDevice(g->dev[k]);
-            (void)hipStreamDestroy(g->stream[k]);
-        }
+        (void)hipSetDevice(g->dev[k]);
+        if (g->stream[k]) (void)hipStreamDestroy(g->stream[k]);
+        if (g->xfer[k]) (void)hipStreamDestroy(g->xfer[k]);
+        for (uint32_t c = 0; c < kMaxChunks; ++c)
+            if (g->done[(size_t)k * kMaxChunks + c]) (void)hipEventDestroy(g->done[(size_t)k * kMaxChunks + c]);
         if (g->ctx[k]) fs_ctx_destroy(g->ctx[k]);
     }
     delete g;
@@ -164,31 +179,59 @@ fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, con
     const uint64_t sb = framesum::plan::slab_bytes(m);
     fs_status st = ensure_slabs(g, sb);
     if (st != FS_SUCCESS) return st;
-    // every shard's kernel on its own device and stream, writing its slab (device 0: in place
-    // in the gather buffer)
-    for (uint32_t k = 0; k < N; ++k) {
-        const uint64_t nk = framesum::plan::shard_count(n, N, k);
-        if (nk == 0) continue;
-        if (!frames[k] || !offsets[k] || !lengths[k])
+    for (uint32_t k = 0; k < N; ++k)
+        if (framesum::plan::shard_count(n, N, k) > 0 && (!frames[k] || !offsets[k] || !lengths[k]))
             return gset(g, FS_E_INVALID, "fs_digest_batch_sharded: null shard pointer");
-        st = fs_digest_batch(g->ctx[k], frames[k], offsets[k], lengths[k], (uint32_t)nk, mtu,
-                             reinterpret_cast<fs_digest*>(g->send[k]), g->send[k] + 8 * m, g->stream[k]);
-        if (st != FS_SUCCESS)
-            return gset(g, st, "fs_digest_batch_sharded: shard " + std::to_string(k) + ": " + fs_last_error(g->ctx[k]));
+    const uint64_t want = (m + kChunkRows - 1) / kChunkRows;
+    const uint64_t R = framesum::plan::chunk_rows(m, (uint32_t)(want < kMaxChunks ? want : kMaxChunks));
+    const uint32_t C = framesum::plan::chunk_count(m, R);
+    hipError_t e = hipSuccess;
+    for (uint32_t c = 0; c < C; ++c) {
+        const uint64_t lo = (uint64_t)c * R, hi = lo + R < m ? lo + R : m;
+        // chunk c of every shard on its own device's compute stream, into its slab (the first
+        // device: in place in the gather buffer)
+        for (uint32_t k = 0; k < N; ++k) {
+            const uint64_t r = framesum::plan::shard_rows_in(n, N, k, lo, hi);
+            if (r == 0) continue;
+            st = fs_digest_batch(g->ctx[k], frames[k], offsets[k] + lo, lengths[k] + lo, (uint32_t)r, mtu,
+                                 reinterpret_cast<fs_digest*>(g->send[k] + 8 * lo), g->send[k] + 8 * m + lo,
+                                 g->stream[k]);
+            if (st != FS_SUCCESS)
+                return gset(g, st, "fs_digest_batch_sharded: shard " + std::to_string(k) + ": " + fs_last_error(g->ctx[k]));
+        }
+        // its transfer waits for those kernels only: the compute streams go on with chunk c+1
+        for (uint32_t k = 0; k < N && e == hipSuccess; ++k) {
+            hipEvent_t ev = g->done[(size_t)k * kMaxChunks + c];
+            e = hipSetDevice(g->dev[k]);
+            if (e == hipSuccess) e = hipEventRecord(ev, g->stream[k]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(g->xfer[k], ev, 0);
+        }
+        if (e != hipSuccess) break;
+        // the chunk's digest and verdict pieces of every other shard to the first device, into
+        // their places in the slabs (point-to-point pairs in one group: the gather of this chunk)
+        ncclResult_t r = ncclGroupStart();
+        for (uint32_t k = 1; k < N && r == ncclSuccess; ++k) {
+            const uint64_t rk = framesum::plan::shard_rows_in(n, N, k, lo, hi);
+            if (rk == 0) continue;
+            uint8_t* at = g->recv + (uint64_t)k * sb;
+            r = ncclSend(g->send[k] + 8 * lo, 8 * rk, ncclUint8, 0, g->comm[k], g->xfer[k]);
+            if (r == ncclSuccess) r = ncclSend(g->send[k] + 8 * m + lo, rk, ncclUint8, 0, g->comm[k], g->xfer[k]);
+            if (r == ncclSuccess) r = ncclRecv(at + 8 * lo, 8 * rk, ncclUint8, (int)k, g->comm[0], g->xfer[0]);
+            if (r == ncclSuccess) r = ncclRecv(at + 8 * m + lo, rk, ncclUint8, (int)k, g->comm[0], g->xfer[0]);
+        }
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess || r2 != ncclSuccess)
+            return gset(g, FS_E_HIP, std::string("fs_digest_batch_sharded: chunk gather: ") +
+                                         ncclGetErrorString(r != ncclSuccess ? r : r2));
+        e = hipSetDevice(g->dev[0]);
+        if (e == hipSuccess)
+            e = framesum::launch_deinterleave(g->recv, N, n, out, status, g->xfer[0], lo * N, hi * N);
+        if (e != hipSuccess) break;
     }
-    // the digests + verdicts of every shard to the first device (the only collective)
-    ncclResult_t r = ncclGroupStart();
-    for (uint32_t k = 0; k < N && r == ncclSuccess; ++k)
-        r = ncclGather(g->send[k], k == 0 ? g->recv : nullptr, sb, ncclUint8, 0, g->comm[k], g->stream[k]);
-    const ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess || r2 != ncclSuccess)
-        return gset(g, FS_E_HIP, std::string("fs_digest_batch_sharded: ncclGather: ") +
-                                     ncclGetErrorString(r != ncclSuccess ? r : r2));
-    hipError_t e = hipSetDevice(g->dev[0]);
-    if (e == hipSuccess) e = framesum::launch_deinterleave(g->recv, N, n, out, status, g->stream[0]);
     for (uint32_t k = 0; k < N && e == hipSuccess; ++k) {
         e = hipSetDevice(g->dev[k]);
         if (e == hipSuccess) e = hipStreamSynchronize(g->stream[k]);
+        if (e == hipSuccess) e = hipStreamSynchronize(g->xfer[k]);
     }
     if (e != hipSuccess) return gset(g, FS_E_HIP, std::string("fs_digest_batch_sharded: ") + hipGetErrorString(e));
     return FS_SUCCESS;

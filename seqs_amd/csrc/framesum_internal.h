@@ -117,8 +117,9 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
                          const FsTablesW* tables_w = nullptr);
 
 // Restore global frame order from nshards gathered round-robin slabs (framesum_plan.h layout):
-// out[i] = slab[i % nshards].digest[i / nshards], status likewise (nullable). framesum_shard.hip.
+// out[i] = slab[i % nshards].digest[i / nshards], status likewise (nullable), for global frames
+// [i0, min(i1, n)) of the n-frame batch. framesum_shard.hip.
 hipError_t launch_deinterleave(const uint8_t* gathered, uint32_t nshards, uint64_t n, void* out, uint8_t* status,
-                               hipStream_t stream);
+                               hipStream_t stream, uint64_t i0 = 0, uint64_t i1 = ~0ull);
 
 }  // namespace framesum

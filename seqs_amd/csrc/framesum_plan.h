@@ -33,6 +33,21 @@ constexpr uint64_t gathered_status_at(uint64_t i, uint32_t nshards, uint64_t m) 
     return (i % nshards) * slab_bytes(m) + 8 * m + i / nshards;
 }
 
+// Chunks of a sharded batch (fs_digest_batch_sharded gathers chunk by chunk, so chunk c's
+// transfer overlaps chunk c+1's kernels): chunk c = local rows [c*R, min((c+1)*R, m)) of every
+// shard, R a multiple of 256 rows (the digest and verdict pieces stay 256-B aligned in the
+// slab). Those rows hold exactly the global frames [c*R*N, min((c+1)*R*N, n)), so the
+// de-interleave of a chunk needs only that chunk's pieces.
+constexpr uint64_t chunk_rows(uint64_t m, uint32_t nchunks) {
+    return nchunks == 0 ? m : ((m + nchunks - 1) / nchunks + 255) / 256 * 256;
+}
+constexpr uint32_t chunk_count(uint64_t m, uint64_t rows) { return rows == 0 ? 0 : (uint32_t)((m + rows - 1) / rows); }
+// shard k's frames in local rows [lo, hi): [lo, min(hi, shard_count))
+constexpr uint64_t shard_rows_in(uint64_t n, uint32_t nshards, uint32_t shard, uint64_t lo, uint64_t hi) {
+    const uint64_t c = shard_count(n, nshards, shard);
+    return (hi < c ? hi : c) > lo ? (hi < c ? hi : c) - lo : 0;
+}
+
 // ---------------------------------------------------------------------------------------
 // Host-staged chunks.
 

@@ -219,7 +219,14 @@ __device__ __forceinline__ void build_tables(const FsTablesRx* __restrict__ tabs
 // Rows.
 
 // A lean row: four Z256 steps and four v_sad_u16, no masks.
+#ifndef FS_RX_DIAG
+#define FS_RX_DIAG 0
+#endif
 __device__ __forceinline__ void lean_row(const Keys& k, u32x4 v, uint32_t (&A)[4], uint32_t& cs) {
+    if (FS_RX_DIAG & 8) {
+        A[0] ^= v.x; A[1] ^= v.y; A[2] ^= v.z; A[3] ^= v.w; cs += v.x;
+        return;
+    }
     A[0] = zrow(A[0], k, v.x);
     A[1] = zrow(A[1], k, v.y);
     A[2] = zrow(A[2], k, v.z);
@@ -869,12 +876,12 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
             if (u >= cu.start) {
                 uint32_t v[4] = {ring[u].x, ring[u].y, ring[u].z, ring[u].w};
                 const int x = cur.rel0 + 64 * u;
-                if (u <= cu.clamp_until) {  // rare: chunks loaded from the frame's page start
+                if (!(FS_RX_DIAG & 4) && u <= cu.clamp_until) {  // rare: chunks loaded from the frame's page start
                     FS_MARK("realign");
                     realign(v, min(max(((int)cur.dP() - 256 * u - 16 * (int)gl) >> 2, 0), 4));
                 }
-                if (u <= cu.cap_until) capture(slot, x, cur.xo(), v);
-                if (u <= cu.mask_until) {
+                if (!(FS_RX_DIAG & 4) && u <= cu.cap_until) capture(slot, x, cur.xo(), v);
+                if (!(FS_RX_DIAG & 4) && u <= cu.mask_until) {
                     FS_MARK("head_row");
                     head_row(keys, v, x, cur.sa(), A, cs);
                 } else {
@@ -888,7 +895,9 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
         }
         // ---- combine the group's piece: W (its pending CRC register) and its sum
         FS_MARK("combine");
-        {
+        if (FS_RX_DIAG & 2) {
+            if (gl == 0u && cur.active()) sts32(wb + kWC + 4u * cur.f(), A[0] ^ A[1] ^ A[2] ^ A[3] ^ cs);
+        } else {
             const uint32_t c4 = pcst(kT4);
             uint32_t U = zt(A[0], c4) ^ A[1];
             U = zt(U, c4) ^ A[2];
@@ -921,7 +930,10 @@ rx_kernel(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offse
         if (cu.last) {
             FS_MARK("finish");
             // ---- the consumer's tile is complete: parse and finish its frames
-            if (lane < 16u && c_tile * 16u + lane < n)
+            if (FS_RX_DIAG & 1) {
+                if (lane < 16u && c_tile * 16u + lane < n)
+                    out[c_tile * 16u + lane] = make_uint2(lds32(wb + kWC + 4u * lane), T0.meta);
+            } else if (lane < 16u && c_tile * 16u + lane < n)
                 finish_frame<kOps>(T0, c_tile * 16u + lane, wb, lane, mtu, frames, wframes, lengths, out, status, tx);
             T0 = T1;
             c_tile = a_tile;

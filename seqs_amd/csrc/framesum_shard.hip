@@ -15,10 +15,10 @@ namespace framesum {
 namespace {
 
 __global__ void __launch_bounds__(256) deinterleave_kernel(const uint8_t* __restrict__ gathered, uint32_t nshards,
-                                                          uint64_t n, uint64_t m, uint2* __restrict__ out,
-                                                          uint8_t* __restrict__ status) {
+                                                          uint64_t i0, uint64_t i1, uint64_t m,
+                                                          uint2* __restrict__ out, uint8_t* __restrict__ status) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    for (uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += stride) {
         out[i] = *reinterpret_cast<const uint2*>(gathered + plan::gathered_digest_at(i, nshards, m));
         if (status) status[i] = gathered[plan::gathered_status_at(i, nshards, m)];
     }
@@ -27,12 +27,13 @@ __global__ void __launch_bounds__(256) deinterleave_kernel(const uint8_t* __rest
 }  // namespace
 
 hipError_t launch_deinterleave(const uint8_t* gathered, uint32_t nshards, uint64_t n, void* out, uint8_t* status,
-                               hipStream_t stream) {
-    if (n == 0) return hipSuccess;
+                               hipStream_t stream, uint64_t i0, uint64_t i1) {
+    if (i1 > n) i1 = n;
+    if (i0 >= i1) return hipSuccess;
     const uint64_t m = plan::shard_rows(n, nshards);
-    uint64_t blocks = (n + 255) / 256;
+    uint64_t blocks = (i1 - i0 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(deinterleave_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, gathered, nshards, n, m,
+    hipLaunchKernelGGL(deinterleave_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, gathered, nshards, i0, i1, m,
                        reinterpret_cast<uint2*>(out), status);
     return hipGetLastError();
 }

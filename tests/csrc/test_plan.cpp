@@ -127,6 +127,30 @@ static void check_shards(uint64_t n, uint32_t N) {
         CHECK(gathered[at / 8] == i);
         CHECK(gst[sat] == (uint8_t)(i & 0x7F));
     }
+    // chunked gather: chunk c's pieces of every slab hold exactly global frames [c R N, (c+1) R N)
+    for (uint32_t nc : {1u, 2u, 3u, 4u, 8u}) {
+        const uint64_t R = chunk_rows(m, nc);
+        const uint32_t C = chunk_count(m, R);
+        CHECK(m == 0 || (R % 256 == 0 && C >= 1 && C <= nc && (uint64_t)C * R >= m && (uint64_t)(C - 1) * R < m));
+        std::vector<uint8_t> hit(n, 0);
+        for (uint32_t c = 0; c < C; ++c) {
+            const uint64_t lo = c * R, hi = std::min<uint64_t>(m, lo + R);
+            uint64_t rows = 0;
+            for (uint32_t k = 0; k < N; ++k) {
+                const uint64_t r = shard_rows_in(n, N, k, lo, hi);
+                CHECK(r <= hi - lo);
+                rows += r;
+                for (uint64_t j = lo; j < lo + r; ++j) {
+                    const uint64_t g = j * N + k;
+                    CHECK(g < n && g >= lo * N && g < std::min<uint64_t>(n, hi * N));
+                    ++hit[g];
+                }
+                CHECK((8 * lo) % 2048 == 0 && lo % 256 == 0);
+            }
+            CHECK(rows == (std::min<uint64_t>(n, hi * N) > lo * N ? std::min<uint64_t>(n, hi * N) - lo * N : 0));
+        }
+        for (uint64_t i = 0; i < n; ++i) CHECK(hit[i] == 1);
+    }
 }
 
 int main() {
