@@ -12,9 +12,9 @@ fs_digest_batch_multi, one context per GPU from ONE process (PCIe-inclusive, not
 batches (> 256 MiB in total) are rotated so the 256 MiB Infinity Cache cannot
 serve them. Multi-GPU (torchrun, one process per GPU, RCCL = torch "nccl"):
 every rank digests its own shard (weak scaling, frame i of the global batch
-on rank i mod N) and the per-frame digests + verdicts are gathered to rank 0
-over RCCL, one gather per group of steps (gather_plan: about half of each stream's steps
-in the region, at most --gather-every), overlapped with the next group's kernels; no other
+on rank i mod N) and the per-frame digests + verdicts go to rank 0 over RCCL in rounds
+(gather_plan: about half the region, at most --gather-every steps; one batch of
+point-to-point transfers per round), overlapped with the next round's kernels; no other
 collective. Rank 0 receives the shards as they are (global frame j*N + r is local frame j
 of rank r: seqs_amd.shard.gather_digests shows the interleave; the bench does not spend a
 rank-0 kernel on it). With N > 1 the same line also carries "c4_strong": the C4 strong-scaled
@@ -59,9 +59,8 @@ def parse():
                         "affinity mask); the 1-thread figure is measured beside it")
     p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather (N>1 diagnostics)")
     p.add_argument("--gather-every", type=int, default=64,
-                   help="N>1: at most this many of a stream's steps per RCCL gather of digests + verdicts to rank "
-                        "0 (gather_plan: about half of each stream's steps in the region, so the region does not "
-                        "end in one drain of all its slabs)")
+                   help="N>1: at most this many steps per gather round (gather_plan: about half the region, so "
+                        "the region does not end in one transfer of all its slabs)")
     p.add_argument("--no-c4", action="store_true", help="N>1: skip the C4 strong-scaled record in the line")
     p.add_argument("--force-gather", action="store_true",
                    help="run the gather path on a single GPU too (a 1-rank process group; a test of the N>1 loop)")
@@ -72,8 +71,7 @@ def parse():
                    help="device pre-warm: when --warmup is below this, (min-warm - warmup) extra untimed "
                         "launches run first, over the streams, without the gather (reported as prewarm_launches)")
     p.add_argument("--kernel", type=int, default=0,
-                   help="fs_ctx_set_kernel variant: 0 automatic, 1 one-pass (end-anchored rows), 2 mixed-length, "
-                        "3 16-lane, 4 one-pass (block-aligned rows)")
+                   help="fs_ctx_set_kernel variant: 0 automatic, 2 mixed-length, 4 one-pass")
     p.add_argument("--streams", type=int, default=5,
                    help="HIP streams the steps rotate over: step i+1's kernel starts on the CUs step i's "
                         "tail frees (every batch is still fully digested). 5 measured best on the 4 hardware "
@@ -113,30 +111,19 @@ def with_room(buf, off, ln, room: int = 4):
 
 
 def gather_plan(steps: int, streams: int, every: int) -> int:
-    """Steps per gather group for a region of `steps` steps over `streams` streams: each stream
-    runs q = ceil(steps / streams) of them; a group holds about half of them (at most `every`),
-    so every stream's first group goes to rank 0 while its second is still being digested and
-    the region ends with at most half of its slabs in flight."""
-    q = (max(1, steps) + max(1, streams) - 1) // max(1, streams)
-    return max(1, min(max(1, every), (q + 1) // 2))
+    """Steps per gather ROUND for a region of `steps` steps: about half the region (at most
+    `every`, at least one step per stream), so the first round goes to rank 0 while the second
+    is still being digested and the region ends with at most half of its slabs in flight."""
+    return max(1, min(max(1, every), max(max(1, streams), (max(1, steps) + 1) // 2)))
 
 
-def gather_schedule(steps: int, streams: int, G: int):
-    """The gathers one region issues, in issue order: (after_step, stream, group, slabs) for every
-    full group (issued right after its last step) and then, at the drain, every stream's partly
-    filled group. Slots of stream s: group g, slab j holds the region's step s + streams*(2*G*k + G*g + j)
-    for some k. (The step loop below follows exactly this schedule; tests/test_bench_plan.py checks it.)"""
-    out = []
-    for i in range(steps):
-        si, q = i % streams, i // streams
-        g, j = (q // G) % 2, q % G
-        if j == G - 1:
-            out.append((i, si, g, G))
-    for si in range(streams):
-        q_end = (steps - si + streams - 1) // streams if steps > si else 0
-        if q_end % G:
-            out.append((steps, si, (q_end // G) % 2, q_end % G))
-    return out
+def gather_schedule(steps: int, R: int):
+    """The gathers one region issues, in issue order: (after_step, buffer, slabs). Step r writes
+    slab r % R of round buffer (r // R) % 2; a round's gather is issued after its last step (or
+    the region's last step), and a buffer is written again only after its previous gather has
+    been waited for. (The step loop below follows exactly this schedule; bench asserts it and
+    tests/test_bench_plan.py checks it.)"""
+    return [(r, (r // R) % 2, r % R + 1) for r in range(steps) if r % R == R - 1 or r == steps - 1]
 
 
 def cpu_model() -> str:
@@ -259,10 +246,12 @@ def main():
     # Output slots (digest words, then verdicts, in one 256-B-aligned slab per slot). Without a
     # gather, step i writes slot i % nslot and slot k is only ever written by stream k (nslot ==
     # ns for ns >= 2; one stream for ns == 1): stream order alone keeps a slot's launches apart.
-    # With the gather, each stream owns 2 groups of G slots for its own consecutive steps; when
-    # a group is full, that stream hands its slabs to rank 0 in one RCCL gather (issued on that
-    # stream, so it waits for that stream's kernels only) while it fills the other group.
-    G = gather_plan(args.steps, ns, args.gather_every) if gather else 1
+    # With the gather, the region's steps go in ROUNDS of R consecutive steps (over all streams):
+    # round k's slabs are one contiguous buffer (2 alternate); after its last step the main stream
+    # joins the others and rank 0 receives every other rank's round buffer by one batch of
+    # point-to-point receives (rank r sends its buffer), overlapped with the next round's kernels.
+    # Rank 0's own slabs stay where its kernels wrote them.
+    R = gather_plan(args.steps, ns, args.gather_every) if gather else 1
     nslot = max(2, ns)
     slab = (9 * n + 255) // 256 * 256
 
@@ -271,79 +260,57 @@ def main():
         return buf[base : base + 8 * n].view(torch.int32).view(n, 2), buf[base + 8 * n : base + 9 * n]
 
     if gather:
-        gbuf = [[torch.empty(G * slab, dtype=torch.uint8, device=dev) for _ in range(2)] for _ in range(ns)]
-        gviews = [[[views(gbuf[st][g], j) for j in range(G)] for g in range(2)] for st in range(ns)]
-        recv = [[[torch.empty_like(gbuf[st][g]) for _ in range(world)] if rank == 0 else None for g in range(2)]
-                for st in range(ns)]
-        # the final partial groups of all streams are packed here (only their written slabs) and
-        # go to rank 0 in ONE gather: a short timed region ends with partial groups only
-        stage = torch.empty(ns * G * slab, dtype=torch.uint8, device=dev)
-        recv_stage = [torch.empty_like(stage) for _ in range(world)] if rank == 0 else None
-        pend = [[None, None] for _ in range(ns)]  # per stream and group: the RCCL work of its latest gather
-        issued = []  # (after_step, stream, group, slabs) of the region's gathers (== gather_schedule)
-        last = {}  # (stream, group) -> ("own" | "all", slabs): which gather delivered it last
+        rbuf = [torch.empty(R * slab, dtype=torch.uint8, device=dev) for _ in range(2)]
+        rviews = [[views(rbuf[b], j) for j in range(R)] for b in range(2)]
+        # rank 0: rank r's round-b slabs at recv[b][r]; 0xFF until received (checked at the end)
+        recv = [[torch.full((R * slab,), 0xFF, dtype=torch.uint8, device=dev) for _ in range(world)]
+                for _ in range(2)] if rank == 0 else None
+        pend = [None, None]  # per buffer: the P2P work of its latest gather
+        issued = []  # (after_step, buffer, slabs) of the region's gathers (== gather_schedule)
+        last = {}  # buffer -> slabs its latest gather carried
     flat = torch.empty(nslot * slab, dtype=torch.uint8, device=dev)
     outs, stats = zip(*[views(flat, k) for k in range(nslot)])
 
-    def step(i: int, r: int):
-        """step i overall, r-th step of its region (the gather groups restart with each region)"""
+    def step(i: int, r: int, K: int):
+        """step i overall, r-th of its region of K steps (the rounds restart with each region)"""
         fb, fo, fl = batches[i % nb]
-        si = r % ns
-        s = streams[si]
+        s = streams[r % ns]
         if not gather:
             run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=s)
             return
-        q = r // ns
-        g, j = (q // G) % 2, q % G
-        with torch.cuda.stream(s):
-            if j == 0 and pend[si][g] is not None:
-                pend[si][g].wait()  # this stream waits until the gather has read group g's slabs
-                pend[si][g] = None
-            o, st = gviews[si][g][j]
-            run_op(fb, fo, fl, mtu=0, out=o, status=st, stream=s)
-            if j == G - 1:
-                pend[si][g] = dist.gather(gbuf[si][g], recv[si][g], dst=0, async_op=True)
-                last[(si, g)] = ("own", G)
-                issued.append((r, si, g, G))
+        b, j = (r // R) % 2, r % R
+        if j == 0 and pend[b] is not None:
+            # buffer b's previous round has been sent: every stream waits for that (stream-side)
+            for st_ in streams:
+                with torch.cuda.stream(st_):
+                    for w in pend[b]:
+                        w.wait()
+            pend[b] = None
+        o, st = rviews[b][j]
+        run_op(fb, fo, fl, mtu=0, out=o, status=st, stream=s)
+        if j == R - 1 or r == K - 1:
+            m = j + 1
+            for st_ in streams[1:]:
+                main_stream.wait_stream(st_)
+            with torch.cuda.stream(main_stream):
+                if rank == 0:
+                    ops = [dist.P2POp(dist.irecv, recv[b][q][: m * slab], q) for q in range(1, world)]
+                else:
+                    ops = [dist.P2POp(dist.isend, rbuf[b][: m * slab], 0)]
+                pend[b] = dist.batch_isend_irecv(ops) if ops else []
+            issued.append((r, b, m))
+            last[b] = m
 
-    def drain(r_end: int):
+    def drain():
         if not gather:
             return
-        # partly filled groups still go to rank 0 (same calls on every rank: r_end is common)
-        part = []
-        for si in range(ns):
-            q_end = (r_end - si + ns - 1) // ns if r_end > si else 0  # steps this stream ran
-            g = (q_end // G) % 2
-            if q_end % G != 0 and pend[si][g] is None:
-                part.append((si, g, q_end % G))  # (stream, group, slabs written in it)
-        if len(part) == ns and len({g for _, g, _ in part}) == 1:
-            # every stream ends in the same partial group: its written slabs, packed on the main
-            # stream once that has joined the others, go to rank 0 in one gather
-            g, m = part[0][1], max(k for _, _, k in part)
-            for si in range(1, ns):
-                streams[0].wait_stream(streams[si])
-            with torch.cuda.stream(streams[0]):
-                for si in range(ns):
-                    stage[si * m * slab : (si + 1) * m * slab].copy_(gbuf[si][g][: m * slab])
-                rv = [r[: ns * m * slab] for r in recv_stage] if rank == 0 else None
-                work = dist.gather(stage[: ns * m * slab], rv, dst=0, async_op=True)
-            for si in range(ns):
-                pend[si][g] = work
-                last[(si, g)] = ("all", m)
-            issued.extend((r_end, si, g, k) for si, g, k in part)
-        else:
-            for si, g, k in part:
-                with torch.cuda.stream(streams[si]):
-                    rv = [r[: k * slab] for r in recv[si][g]] if rank == 0 else None
-                    pend[si][g] = dist.gather(gbuf[si][g][: k * slab], rv, dst=0, async_op=True)
-                last[(si, g)] = ("own", k)
-                issued.append((r_end, si, g, k))
-        for si in range(ns):
-            for g in range(2):
-                if pend[si][g] is not None:
-                    with torch.cuda.stream(streams[si]):
-                        pend[si][g].wait()
-                    pend[si][g] = None
+        for b in range(2):
+            if pend[b] is not None:
+                for st_ in streams:
+                    with torch.cuda.stream(st_):
+                        for w in pend[b]:
+                            w.wait()
+                pend[b] = None
 
     # device pre-warm (setup, not steps): throughput settles only after several hundred launches
     prewarm = max(0, args.min_warm - args.warmup)
@@ -354,8 +321,8 @@ def main():
         run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=streams[i % ns])
     torch.cuda.synchronize()
     for i in range(args.warmup):
-        step(i, i)
-    drain(args.warmup)
+        step(i, i, args.warmup)
+    drain()
     torch.cuda.synchronize()
     if gather:
         last.clear()  # the checks below cover the timed region's gathers
@@ -367,8 +334,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i, i)
-    drain(args.steps)
+        step(args.warmup + i, i, args.steps)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -379,13 +346,14 @@ def main():
         elapsed = float(t.item())
 
     if gather:
-        assert issued == gather_schedule(args.steps, ns, G), "the region's gathers differ from gather_schedule"
-    if gather and rank == 0:
-        # every group's latest gather delivered rank 0's own slabs intact (a check of the loop)
+        assert issued == gather_schedule(args.steps, R), "the region's gathers differ from gather_schedule"
+    if gather and rank == 0 and world > 1:
+        # every other rank's latest round arrived (valid frames: all verdicts 0, where 0xFF was)
         torch.cuda.synchronize()
-        for (si, g), (how, m) in last.items():
-            got = recv[si][g][0][: m * slab] if how == "own" else recv_stage[0][si * m * slab : (si + 1) * m * slab]
-            assert torch.equal(got, gbuf[si][g][: m * slab]), "gathered digests differ from rank 0's own"
+        for b, m in last.items():
+            for q in range(1, world):
+                got = recv[b][q][: m * slab].view(m, slab)[:, 8 * n : 9 * n]
+                assert int(got.max().item()) == 0, f"rank {q}'s round-{b} slabs did not arrive"
 
     # ---- kernel-only timing with HIP events on the launch stream (roofline.achieved): one event
     # pair around K back-to-back launches on one stream (no overlap with another launch), so the
@@ -400,6 +368,7 @@ def main():
         k1.record(main_stream)
     torch.cuda.synchronize()
     k_avg_ms = k0.elapsed_time(k1) / args.steps
+    engine_last_kernel = engine.last_kernel()
 
     total_bytes = bytes_per_batch * args.steps * world
     value = total_bytes / elapsed / GIB
@@ -457,7 +426,9 @@ def main():
                                 "the line two neighbouring frames share is fetched twice (~8.4% on C2); "
                                 "traffic_calibrated divides that pattern factor out (the kernel's excess beyond it)"
                 if traffic is not None else None,
-                "kernel": "digest_kernel",
+                "kernel": {0: "automatic: digest_kernel_a (one-pass) for uniform batches, digest_kernel_ab for mixed",
+                           2: "digest_kernel_ab (mixed-length)", 4: "digest_kernel_a (one-pass)"}.get(args.kernel),
+                "kernel_chosen": {2: "digest_kernel_ab", 4: "digest_kernel_a"}.get(engine_last_kernel),
                 "kernel_avg_us": round(k_avg_ms * 1e3, 3),
                 "kernel_timing": "HIP events around K back-to-back launches on the launch stream",
                 "algorithmic_bytes_per_launch": bytes_per_batch,
@@ -467,7 +438,7 @@ def main():
     engine.close()
     del batches, flat
     if gather:
-        del gbuf, recv, stage, recv_stage
+        del rbuf, rviews, recv
     if world > 1 and args.config == "c2" and args.op == "digest" and not args.no_c4:
         # the C4 strong-scaled record beside the weak-scaled C2 value (same steps / warmup)
         torch.cuda.empty_cache()
@@ -658,7 +629,7 @@ def run_c4(args, world, rank, local, dev, frames):
                 "unit": "GB/s",
                 "frac": round(bytes_local / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": None,
-                "kernel": "digest_kernel",
+                "kernel": "automatic choice (uniform 1500-B shards: digest_kernel_a, the one-pass kernel)",
                 "kernel_avg_us": round(k_ms * 1e3, 3),
                 "frac_mode": "rank 0's shard kernel, single stream",
             },

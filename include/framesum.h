@@ -216,18 +216,15 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
                           uint8_t* status, void* stream);
 
 /* Kernel variant of a context's launches. The engine has two: a one-pass kernel
- * for batches of similar frame lengths, and one that splits long frames into
- * 768-byte pieces when a tile of 16 frames mixes very different lengths. By
- * default (variant 0) every launch reports whether its batch had such tiles and
- * the next launch picks accordingly (the one-pass choice reads each frame as the
- * 64-byte blocks that hold it). 1 forces the one-pass kernel with rows anchored at
- * the frame end, 2 the mixed one, 3 the 16-lane kernel (256-byte rows per frame;
- * DESIGN.md §3.8), 4 the one-pass kernel with block-aligned rows, 5 the same as
- * two 8-wave workgroups per CU (digest and FCS verify; the TX fill runs 4). Results
- * are identical in every case; only the speed differs. */
+ * for batches of similar frame lengths (each frame read as the 64-byte blocks that
+ * hold it), and one that splits long frames into 768-byte pieces when a tile of 16
+ * frames mixes very different lengths. By default (variant 0) every launch reports
+ * whether its batch had such tiles and the next launch picks accordingly. 2 forces
+ * the mixed-length kernel, 4 the one-pass kernel; any other value is FS_E_INVALID.
+ * Results are identical in every case; only the speed differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
-/* The variant (1..5, as above) the context's latest launch ran; 0 before its first
+/* The variant (2 or 4, as above) the context's latest launch ran; 0 before its first
  * launch, FS_E_INVALID for a null context. With variant 0 a context's first 16
  * launches run the mixed-length kernel (2), which keeps itself chosen while it
  * meets mixed tiles; uniform traffic then moves to the one-pass kernel (4). */

@@ -47,9 +47,6 @@ struct fs_ctx {
     int device = 0;
     int num_cus = 0;
     FsTables* d_tables = nullptr;
-    framesum::FsTablesW* d_tables_w = nullptr;
-    framesum::FsTablesRx* d_tables_rx = nullptr;
-    int rx_grid = 1;  // streaming kernel: workgroups per CU (FS_RX_GRID)
     // fault injection for the host-staged pipeline's tests (FS_FAULT_CHUNK=k: fs_digest_batch_host
     // fails with FS_E_NOMEM at chunk k, after the earlier chunks' work and chunk k's copy are queued)
     long fault_chunk = -1;
@@ -57,6 +54,7 @@ struct fs_ctx {
     volatile uint32_t* h_report = nullptr;
     uint32_t* d_report = nullptr;
     int force_kernel = 0;  // fs_ctx_set_kernel
+    uint32_t next_launch_id = 1;  // the ids this context's launches report under (launch_digest)
     HostSlot slot[kHostSlots];
     hipStream_t copy_stream = nullptr, compute_stream = nullptr;
     hipStream_t copy_stream2 = nullptr;  // the odd chunks' frame copies
@@ -153,15 +151,13 @@ fs_status quiesce_host_streams(fs_ctx* ctx) {
     return FS_SUCCESS;
 }
 
-// One launch of the context's kernel choice (variant 6: the streaming kernel).
+// One launch of the context's kernel choice.
 hipError_t launch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                   uint32_t mtu, fs_digest* out, uint8_t* status, hipStream_t stream, framesum::FsOp op,
                   uint8_t* wframes, uint32_t tx) {
-    if (ctx->force_kernel == 6)
-        return framesum::launch_rx(frames, offsets, lengths, n, mtu, ctx->d_tables_rx, out, status, stream, ctx->num_cus,
-                                   ctx->rx_grid, (int)op, wframes, tx);
     return framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status, stream, ctx->num_cus,
-                                   ctx->h_report, ctx->d_report, ctx->force_kernel, op, wframes, tx, ctx->d_tables_w);
+                                   ctx->h_report, ctx->d_report, &ctx->next_launch_id, ctx->force_kernel, op, wframes,
+                                   tx);
 }
 
 }  // namespace
@@ -203,20 +199,6 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
     e = hipMalloc(&ctx->d_tables, sizeof(FsTables));
     if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, h, sizeof(FsTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        framesum::FsTablesW* hw = new (std::nothrow) framesum::FsTablesW;
-        if (!hw) e = hipErrorOutOfMemory;
-        if (hw) framesum::build_tables_w(hw);
-        if (e == hipSuccess) e = hipMalloc(&ctx->d_tables_w, sizeof(framesum::FsTablesW));
-        if (e == hipSuccess) e = hipMemcpy(ctx->d_tables_w, hw, sizeof(framesum::FsTablesW), hipMemcpyHostToDevice);
-        delete hw;
-    }
-    if (e == hipSuccess) {
-        framesum::FsTablesRx hr;
-        framesum::build_tables_rx(&hr);
-        e = hipMalloc(&ctx->d_tables_rx, sizeof(framesum::FsTablesRx));
-        if (e == hipSuccess) e = hipMemcpy(ctx->d_tables_rx, &hr, sizeof(framesum::FsTablesRx), hipMemcpyHostToDevice);
-        const char* g = std::getenv("FS_RX_GRID");
-        if (g && std::atoi(g) == 2) ctx->rx_grid = 2;
         const char* fc = std::getenv("FS_FAULT_CHUNK");
         if (fc && *fc) ctx->fault_chunk = std::atol(fc);
     }
@@ -275,8 +257,6 @@ fs_status fs_ctx_destroy(fs_ctx* ctx) {
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     if (ctx->h_report) (void)hipHostFree(const_cast<uint32_t*>(ctx->h_report));
     (void)hipFree(ctx->d_tables);
-    (void)hipFree(ctx->d_tables_w);
-    (void)hipFree(ctx->d_tables_rx);
     delete ctx;
     return FS_SUCCESS;
 }
@@ -587,7 +567,8 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
     ctx->err.clear();
-    if (variant < 0 || variant > 6) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0..6");
+    if (variant != 0 && variant != 2 && variant != 4)
+        return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0 (automatic), 2 or 4");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
 }

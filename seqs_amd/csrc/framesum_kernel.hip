@@ -1,49 +1,49 @@
-// framesum digest kernel — CDNA4 / gfx950.
+// framesum digest kernels — CDNA4 / gfx950.
 //
 // One fused pass per frame over HBM computes
 //   * the IEEE CRC-32 of frame[0:len)                     (new: SURVEY.md §0.1)
 //   * IPv4Header.CalculateChecksum() of frame[14:34]      (eth/headers.go:333-340)
 //   * the TCP/UDP checksum RecvEth verifies + its verdict (stacks/portstack.go:163-308,
 //     eth/headers.go:382-393, :510-527, arithmetic of eth/crc.go:13-84)
+// and, as the TX fill (fs_fill_batch), writes the checksums and/or the FCS into the frames.
 //
-// Work decomposition:
-//   * a wave owns a TILE of 16 frames; each frame gets a 4-lane GROUP.
-//   * a frame is cut into 64-byte ROWS anchored at its (dword-rounded) END, so the
-//     head row is the partial one; lane l of the group loads dwords [4l, 4l+4) of
-//     every row with one global_load_dwordx4 (16 B/lane), kPrefetch rows ahead.
-//   * LEAN rows: every row except the first H of a tile (H = 1 or 2 for a batch of
-//     equal lengths) is consumed with no per-row mask at all. The head rows (bytes
-//     before the frame, the CRC init on frame dwords 0/1) take the masked path. The
-//     up to 3 bytes past the frame end that the dword rounding reads are not masked
-//     in the loop: their CRC contribution is XOR-ed out of the combine and their sum
-//     subtracted at the finish (both linear).
-//   * CRC: each lane keeps 4 independent dword STREAMS; a stream's successive
-//     dwords are 64 B apart, so its Horner step is  A <- Z64(A) ^ w  with Z64 a
-//     fixed GF(2) linear map evaluated by 4 byte-table lookups in LDS. After the
-//     last row the 16 streams of a frame are combined in 3 dependent lookups
-//     (U = Z12(A0)^Z8(A1)^Z4(A2)^A3 per lane, Z_(16(3-l)) per lane l + DPP
-//     quad xor, then a final Z_(4-t) that also removes the t <= 3 zero bytes
-//     the dword rounding appended). Leading zero rows do not change a zero-init CRC; the
-//     CRC init is applied by XOR-ing the frame's first 4 bytes with 0xFF.
-//   * one's-complement sum: the same registers feed v_sad_u16 (acc += lo16 + hi16,
-//     one op per dword; congruent mod 65535 to the byte-swapped big-endian word
-//     sum) over every frame byte; the header parse computes, in the same domain,
-//     the sums of the Ethernet + IP header bytes, of the excluded words and of the
-//     Ethernet padding (vectorised over the group's 4 lanes) and the pseudo-header,
-//     and the finish folds with a positive offset so RecvEth's Sum16 result (incl.
-//     the 0x0000 / 0xFFFF edge) is reproduced bit for bit.
-//   * the frame's first 32 dwords reach a per-group LDS header slot by dword LDS-DMA
-//     issued with the tile's first rows (no per-row header capture); the parse runs
-//     after the first block of rows, behind the ring's loads.
-//   * LDS tables: the hot Z64 table is stored as 8 copies per byte table in an
-//     [entry][table*8+copy] layout, 256 B per entry. Lane L = c + 8h of a 32-lane
-//     bank group reads table (k+h)&3 in its k-th lookup, so the 32 lanes hit 32
-//     distinct banks: conflict-free ds_read_b32 for any data. One v_perm_b32 forms
-//     the LDS address (entry byte | per-lane slot byte).
+// Two kernels; launch_digest (bottom) picks one per launch, never changing a result:
+//   * digest_kernel_a, the ONE-PASS kernel (batches of similar lengths, e.g. C2): a 16-wave
+//     workgroup per CU, persistent; a wave owns a TILE of 16 frames, each frame a 4-lane GROUP.
+//     Rows are the 64-B blocks (half 128-B lines) that hold the frame, the last one ending on
+//     the block boundary after the frame end: lane l of the group loads dwords
+//     [4l, 4l+4) of every row with one global_load_dwordx4, kRingA rows ahead. Rows before the
+//     frame's first block reload that block (no byte before the frame's page is touched). The
+//     frame's first 3 blocks are copied from the first rows into a per-wave LDS header slot as
+//     they are consumed (header capture: no extra load), and the parse reads them there.
+//   * digest_kernel_ab, the MIXED-LENGTH kernel (e.g. C3): the same rows end-anchored at the
+//     frame's dword-rounded end, header slots by dword LDS-DMA, and tiles whose frames differ
+//     widely in length cut their long frames into 768-B PIECES spread over the groups the short
+//     frames leave idle (mode B), combined per frame with Z768 Horner steps.
+// Both:
+//   * LEAN rows carry no mask. The head rows (bytes before the frame, the CRC init on frame
+//     dwords 0/1) take the masked path; bytes past the frame end in the last row are masked
+//     (one-pass) or removed linearly at the combine (mixed).
+//   * CRC: each lane keeps 4 independent dword STREAMS; a stream's successive dwords are 64 B
+//     apart, so its Horner step is  A <- Z64(A) ^ w  with Z64 a fixed GF(2) linear map evaluated
+//     by 4 byte-table lookups in LDS. After the last row the 16 streams of a frame are shifted
+//     to the frame end and XOR-ed over the group (DPP). Leading zero rows do not change a
+//     zero-init CRC; the init is applied by XOR-ing the frame's first 4 bytes with 0xFF.
+//   * one's-complement sum: the same registers feed v_sad_u16 (acc += lo16 + hi16, one op per
+//     dword; congruent mod 65535 to the byte-swapped big-endian word sum) over every frame byte;
+//     the header parse computes, in the same domain, the sums of the Ethernet + IP header bytes,
+//     of the excluded words and of the Ethernet padding (vectorised over the group's 4 lanes)
+//     and the pseudo-header, and the finish folds with a positive offset so RecvEth's Sum16
+//     result (incl. the 0x0000 / 0xFFFF edge) is reproduced bit for bit.
+//   * LDS tables, built in place by VALU from their GF(2) bases (FsTables): the hot Z64 table
+//     as 8 copies per byte table in an [entry][table*8+copy] layout, 256 B per entry. Lane
+//     L = c + 8h of a 32-lane bank group reads table (k+h)&3 in its k-th lookup, so the 32
+//     lanes hit 32 distinct banks: conflict-free ds_read_b32 for any data. One v_perm_b32 forms
+//     the LDS address (entry byte | per-lane slot byte). The plain [4][256] tables (combine,
+//     finish) follow.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <atomic>
 #include <type_traits>
 
 #include "framesum_internal.h"
@@ -54,104 +54,16 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
-#ifndef FS_PREFETCH
-#define FS_PREFETCH 6
-#endif
-#ifndef FS_TXDIAG
-#define FS_TXDIAG 0  // diagnostic builds only: 1 skips the fill's CRC correction, 2 its field stores, 4 the FCS stores
-#endif
-#ifndef FS_DIAG
-#define FS_DIAG 0  // diagnostic builds only (wrong results): 1 no header DMA, 2 no plain-table DMA, 16 no parse,
-                   // 32 no finish (one-pass kernel)
-#endif
-#ifndef FS_AGE_PRIO
-#define FS_AGE_PRIO 2  // one-pass kernel: a SIMD's later-started waves get the higher issue priority: 1 four levels
-                       // (wave >> 2), 2 two levels (wave >> 3; round 2: -0.35..-0.55 us per launch, whole job level)
-#endif
-#ifndef FS_PRE_PRIO
-#define FS_PRE_PRIO 0  // s_setprio(3) through the preamble (one-pass kernel)
-#endif
-#ifndef FS_TILE_MAP
-#define FS_TILE_MAP 1  // first tile of a wave: 0 block-major, 1 wave-major, 2 a contiguous 1/8 per XCD
-#endif
-#ifndef FS_EARLY_TABLES
-#define FS_EARLY_TABLES 1  // the plain-table DMA right behind the descriptor loads (0: after the geometry)
-#endif
-#ifndef FS_ROWS_FIRST
-#define FS_ROWS_FIRST 0  // one-pass kernel: the first tile's rows before its header DMA (measured: within noise)
-#endif
-#ifndef FS_LATE_REPORT
-#define FS_LATE_REPORT 0  // one-pass kernel: the mixed-length report after the parse (measured slower)
-#endif
-#ifndef FS_EARLY_BARRIER
-#define FS_EARLY_BARRIER 0  // one-pass kernel: the tables barrier right after the descriptors, before the geometry
-                           // and the first rows (measured 1.4 us slower on C2)
-#endif
-#ifndef FS_HDR_CAPTURE
-#define FS_HDR_CAPTURE 1  // block-aligned one-pass kernel: header slots captured from the first rows (no header DMA)
-#endif
-#ifndef FS_HDR_AL
-#define FS_HDR_AL 32  // block-aligned one-pass kernel: header slot dwords (16 or 32; 16 measured within noise)
-#endif
-#ifndef FS_CHAIN
-#define FS_CHAIN 0  // block-aligned one-pass kernel: chained tiles (the ring runs on across a wave's
-                    // tiles); parity-green, C4 within noise of the unchained kernel
-#endif
-#ifndef FS_REPORT_AFTER_ROWS
-#define FS_REPORT_AFTER_ROWS 1  // block-aligned one-pass kernel: the first tile's mixed-length report check after
-                                // its first rows are issued (0: before them)
-#endif
-#ifndef FS_EARLY_ROWS
-#define FS_EARLY_ROWS 1  // block-aligned one-pass kernel: the first tile's H and capture flag after its first rows' issue
-#endif
-#ifndef FS_TABLES_BARRIER
-#define FS_TABLES_BARRIER 0  // one-pass kernel: 1 = the tables barrier right after the in-place build, before the descriptors'
-                             // wait (measured 1.3 us slower on C2: the waves then issue their first rows in one burst)
-#endif
-#ifndef FS_AB_ROWS_FIRST
-#define FS_AB_ROWS_FIRST 1  // mixed-length kernel: the first tile's rows before its header DMA
-#endif
-#ifndef FS_FIN_PRIO
-#define FS_FIN_PRIO 0  // one-pass kernel: s_setprio(3) for the combine and the finish
-#endif
-#ifndef FS_PLAIN_VALU
-#define FS_PLAIN_VALU 1  // the plain tables built in place by VALU from their bases (0: copied by LDS-DMA)
-#endif
-#ifndef FS_A2_VALU
-#define FS_A2_VALU 0  // two-workgroups-per-CU kernel: 1 = region A built in place by VALU (measured 3% slower than
-                      // the LDS-DMA copy: its upper-half plain tables take 8-way conflicted ds_write_b32)
-#endif
-#ifndef FS_PRIO_MIN
-#define FS_PRIO_MIN 36  // ... for tiles of more rows than this
-#endif
-#ifndef FS_AGE_PRIO_AB
-#define FS_AGE_PRIO_AB 2  // mixed-length kernel: 2 = the one-pass kernel's two-level age priority (C3 whole job +2.6%)
-#endif
-#ifndef FS_PRIO_AB
-#define FS_PRIO_AB 0  // ... in the mixed-length kernel (round 2: off, C3 -0.6 us alone and +1.6% whole job)
-#endif
-#ifndef FS_PRIO
-#define FS_PRIO 1  // progress-based s_setprio per block of rows (one-pass kernel)
-#endif
-
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 16;
 constexpr int kThreads = kWave * kWavesPerBlock;
 constexpr int kFramesPerTile = 16;
 constexpr int kRowDwords = 16;
-constexpr int kPrefetch = FS_PREFETCH;  // the mixed-length kernel's ring (a divisor of kPieceRows)
-#ifndef FS_PREFETCH_A
-#define FS_PREFETCH_A 6
-#endif
-constexpr int kPrefetchA = FS_PREFETCH_A;  // the one-pass kernel's ring
-#ifndef FS_PREFETCH_AL
-#define FS_PREFETCH_AL 5
-#endif
+constexpr int kPrefetch = 6;  // the mixed-length kernel's ring (a divisor of kPieceRows)
 // ... with block-aligned rows: an MTU frame (1500 B) spans 24 or 25 blocks, so a tile's rows
 // are a multiple of 5 with no padding row
-constexpr int kPrefetchAl = FS_PREFETCH_AL;
-template <bool kAl>
-constexpr int kRingA = kAl ? kPrefetchAl : kPrefetchA;
+constexpr int kRingA = 5;  // the one-pass kernel's ring
+constexpr int kPrioMinRows = 36;  // the one-pass kernel's progress-based priority: tiles of more rows than this
 
 // Header slots: frame dwords [0, 32) of each group's frame, written by 8 dword LDS-DMA
 // instructions per wave in the layout [x >> 2][group][x & 3] (256 B per instruction),
@@ -187,53 +99,10 @@ static_assert(kWaveScratchBytes >= 3u * 256u, "a parked parse (12 dwords x 16 fr
 static_assert(kPieceRows % kPrefetch == 0, "a piece is whole blocks of rows");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kTablesLdsBytes == kLdsTables, "FsTables is the LDS image of the tables");
-constexpr uint32_t kPlainChunk0 = 65536 / 1024;                     // first 1-KB piece of the plain tables in FsTables
-constexpr uint32_t kPlainChunks = kLdsRegionA / 1024;               // 40 pieces, to LDS [0, 40 KB)
-constexpr uint32_t kDmaPerWave = (kPlainChunks + kWavesPerBlock - 1) / kWavesPerBlock;
-
-// ---- LDS map of the 16-lane kernel (digest_kernel_w, below): the 11 plain tables of FsTablesW,
-// region A (Z_244 and Z_4), 16 x 1-KB header slots (16 frame dwords per frame), 16 x per-wave scratch.
-constexpr uint32_t kW_Z16 = 0, kW_Z32 = 4096, kW_Z48 = 8192, kW_Z64 = 12288, kW_Z128 = 16384, kW_Z192 = 20480;
-constexpr uint32_t kW_Zfin = 24576, kW_Z1024 = 40960;
-constexpr uint32_t kW_RegionA = kTablesWPlainBytes;
-constexpr int kHdrDwW = 16;
-constexpr uint32_t kHdrWaveW = 4u * kHdrDwW * kFramesPerTile;  // 1 KB
-constexpr uint32_t kW_Hdr = kTablesWLdsBytes;
-constexpr uint32_t kW_Wave = kW_Hdr + kWavesPerBlock * kHdrWaveW;
-// per-wave scratch: parked parse (12 dwords x 16 frames, [k >> 2][frame][k & 3]), the passes'
-// {Y, csum} per frame, and two super-tile geometry buffers (the one being consumed, the next)
-constexpr uint32_t kW_Park = 0, kW_Ycs = 768, kW_Geo = 896, kW_GeoBytes = 320;
-constexpr uint32_t kW_GeoOrder = 256, kW_GeoP = 272, kW_GeoH = 288, kW_GeoNpass = 304;
-// the next super-tile's descriptors, by one dword LDS-DMA: 16 offsets (u64), 16 lengths (u32)
-constexpr uint32_t kW_Desc = kW_Geo + 2 * kW_GeoBytes, kW_DescLen = 128;
-constexpr uint32_t kW_WaveBytes = kW_Desc + 256;
-constexpr uint32_t kW_LdsBytes = kW_Wave + kWavesPerBlock * kW_WaveBytes;
-static_assert(kW_LdsBytes <= 160 * 1024, "LDS budget (16-lane kernel)");
-static_assert(kW_Zfin + 16384 == kW_Z1024 && kW_Z1024 + 4096 == kTablesWPlainBytes, "FsTablesW plain layout");
-static_assert(kW_RegionA < 65536, "ds_read offset field");
-constexpr uint32_t kLdsAlloc = kLdsBytes > kW_LdsBytes ? kLdsBytes : kW_LdsBytes;
 
 // The workgroup's LDS image (static allocation of the digest kernels). Namespace scope, so the
 // out-of-line parse routine addresses it as LDS (ds_read), not through a flat pointer.
-__shared__ __attribute__((aligned(16))) char g_lds[kLdsAlloc];
-
-// ---- LDS map of the two-workgroups-per-CU kernel (digest_kernel_a with LayA2): 8 waves and
-// 80 KB per workgroup, so that a CU holds two and a launch's workgroups start while the previous
-// launch's still stream. [0, 64 KB): FsTables::region_a as it is, by LDS-DMA -- each 256-B entry
-// row holds Z64's 8 replicated copies (bytes 0..127, the row lookups' conflict-free layout) and,
-// in bytes 128..255, the 8 plain tables the combine and the finish use, XOR-swizzled by the entry
-// (kA2Plain); [64 KB, 80 KB): 8 captured header slots of 2 KB (the frame's first 2 blocks).
-constexpr int kA2Waves = 8;
-constexpr uint32_t kA2Hdr = 65536;
-constexpr uint32_t kA2HdrStride = 2048;
-constexpr uint32_t kA2Bytes = kA2Hdr + kA2Waves * kA2HdrStride;
-static_assert(kA2Bytes == 80u * 1024u, "two workgroups per CU");
-__shared__ __attribute__((aligned(16))) char g_lds2[kA2Bytes];
-template <bool kL2>
-__device__ __forceinline__ char* lds_image() {
-    if constexpr (kL2) return g_lds2;
-    else return g_lds;
-}
+__shared__ __attribute__((aligned(16))) char g_lds[kLdsBytes];
 
 #ifdef FS_STAMPS
 // Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
@@ -292,15 +161,9 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
-// Z_stride(a) ^ w from replicated region A (Z64 in the 4-lane kernels, Z256 in the 16-lane one).
-// Conflict-free.
+// Z64(a) ^ w from replicated region A. Conflict-free.
 template <uint32_t kRegion = kLdsRegionA>
 __device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const LaneKeys& k, uint32_t w) {
-    if (FS_DIAG & 8) {  // diagnostic: the address VALU without the LDS reads (wrong CRC)
-        const uint32_t u0 = __builtin_amdgcn_perm(a, k.cvec, k.sel[0]), u1 = __builtin_amdgcn_perm(a, k.cvec, k.sel[1]);
-        const uint32_t u2 = __builtin_amdgcn_perm(a, k.cvec, k.sel[2]), u3 = __builtin_amdgcn_perm(a, k.cvec, k.sel[3]);
-        return xor3(xor3(u0, u1, u2), u3, w);
-    }
     uint32_t t0 = lds32(lds, kRegion + __builtin_amdgcn_perm(a, k.cvec, k.sel[0]));
     uint32_t t1 = lds32(lds, kRegion + __builtin_amdgcn_perm(a, k.cvec, k.sel[1]));
     uint32_t t2 = lds32(lds, kRegion + __builtin_amdgcn_perm(a, k.cvec, k.sel[2]));
@@ -341,11 +204,6 @@ __device__ __forceinline__ uint32_t range_mask(int k, int a0, int a1) {
 // A lean row: four Z_stride steps and four v_sad_u16, no masks.
 template <uint32_t kRegion = kLdsRegionA>
 __device__ __forceinline__ void lean_row(const char* lds, const LaneKeys& k, u32x4 v, uint32_t (&A)[4], uint32_t& cs) {
-    if (FS_DIAG & 4) {  // diagnostic: no table lookups (wrong CRC; the loads and the sum stay)
-        A[0] = xor3(A[0], v.x, A[1]); A[1] ^= v.y; A[2] ^= v.z; A[3] ^= v.w;
-        cs = sad16(v.x, cs); cs = sad16(v.y, cs); cs = sad16(v.z, cs); cs = sad16(v.w, cs);
-        return;
-    }
     A[0] = zrep<kRegion>(lds, A[0], k, v.x);
     A[1] = zrep<kRegion>(lds, A[1], k, v.y);
     A[2] = zrep<kRegion>(lds, A[2], k, v.z);
@@ -615,14 +473,12 @@ __device__ __forceinline__ Parsed unpark_parsed(const char* lds, uint32_t hw, ui
 // call saves nothing). Every lane takes part: group-vectorised sums over the header slot
 // (the bytes [0, off) of the Ethernet + IP headers; the Ethernet padding [end, len) when it
 // lies in the slot), then the parser lane's gates and corrections, parked in LDS.
-// `pk`: where the parse result is parked (the 4-lane kernels park it in the header slot itself).
-// parse_tile_body: the same, inlined (the 16-lane kernel's single parse site: a call there would
-// end in a vmcnt(0) that drains the row ring).
-template <uint32_t kOps, int kSlotDw = kHdrDwords, bool kL2 = false>
-__device__ __forceinline__ void parse_tile_body(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
-                                                uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk,
-                                                uint32_t xo = 0u) {
-    const char* lds = lds_image<kL2>();
+// `pk`: where the parse result is parked (the header slot itself).
+template <uint32_t kOps, int kSlotDw = kHdrDwords>
+__device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
+                                                     uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk,
+                                                     uint32_t xo = 0u) {
+    const char* lds = g_lds;
     const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 3, xo));
     const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
     const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, grp, sa, 4, xo)) >> 16;
@@ -639,13 +495,7 @@ __device__ __forceinline__ void parse_tile_body(uint32_t hw, uint32_t grp, uint3
         if (pad_in_slot) pad = (int64_t)ps;
     }
     if (parser)
-        park_parsed<kOps>(lds_image<kL2>(), pk, grp, parse_frame<kOps, kSlotDw>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs, xo));
-}
-template <uint32_t kOps, int kSlotDw = kHdrDwords, bool kL2 = false>
-__device__ __attribute__((noinline)) void parse_tile(uint32_t hw, uint32_t grp, uint32_t gl, uint32_t sa, uint32_t len,
-                                                     uint32_t mtu, const uint32_t* fbs, bool parser, uint32_t pk,
-                                                     uint32_t xo = 0u) {
-    parse_tile_body<kOps, kSlotDw, kL2>(hw, grp, gl, sa, len, mtu, fbs, parser, pk, xo);
+        park_parsed<kOps>(g_lds, pk, grp, parse_frame<kOps, kSlotDw>(lds, hw, grp, sa, len, mtu, hsum, pad, fbs, xo));
 }
 
 // Final L4 checksum + verdict (parser lane) once the streamed sum is known.
@@ -694,7 +544,7 @@ __device__ __forceinline__ void st8(uint8_t* p, uint32_t v) { *p = (uint8_t)v; }
 // The parser lane's finish of one frame: CRC-32 from the combined register Y, L4 checksum and
 // verdict from the streamed sum `cs` and the parked parse, then the op's writes and stores.
 // `len` is the frame length the rows streamed (kOpsFcs: without the FCS).
-// The table layout of the 4-lane kernels, for the finish (LayoutW: the 16-lane kernel).
+// The table layout the finish reads.
 struct LayoutA {
     static constexpr uint32_t kZfin = kLdsZfin;
     __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift(lds, v, k); }
@@ -738,19 +588,17 @@ __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, u
             // the CRC of the written frame differs from the streamed one by the CRC (zero init)
             // of the two 16-bit XOR deltas: Z_(len-p2)( Z_(p2-24)(d_ip) ^ d_l4 ), d as LE bytes
             const uint32_t ipc = P.ip_csum, old_ip = P.aux & 0xffffu, p2 = P.aux >> 16;
-            if (!(FS_TXDIAG & 1)) {
+            {
                 const uint32_t d = L::shift(lds, bswap16(old_ip ^ ipc), p2 - 24u) ^ bswap16(P.stored ^ l4);
                 crcv ^= L::shift(lds, d, len - p2);
             }
-            if (!(FS_TXDIAG & 2)) {
-                st8(wf + 24, ipc >> 8);
-                st8(wf + 25, ipc);
-                st8(wf + p2, l4 >> 8);
-                st8(wf + p2 + 1, l4);
-            }
+            st8(wf + 24, ipc >> 8);
+            st8(wf + 25, ipc);
+            st8(wf + p2, l4 >> 8);
+            st8(wf + p2 + 1, l4);
             verdict = V_OK;  // the written field now holds the computed checksum
         }
-        if ((tx & kTxAppend) && !(FS_TXDIAG & 4)) {
+        if (tx & kTxAppend) {
             st8(wf + len, crcv);
             st8(wf + len + 1, crcv >> 8);
             st8(wf + len + 2, crcv >> 16);
@@ -1003,7 +851,7 @@ struct TileA {
     int H;      // wave-uniform: leading rows that take the masked path
     uint32_t ph;  // block-aligned rows: absolute 64-B block phase (in dwords) of frame dword 0
     int r0f;      // block-aligned rows: the row of the frame's first block (large for an empty group)
-    int cap;      // wave-uniform: every frame's first 3 (LayA2: 2) blocks lie in the first block of rows (captured there)
+    int cap;      // wave-uniform: every frame's first 3 blocks lie in the first block of rows (captured there)
     // derived per use (they would otherwise hold VGPRs across the row loop)
     __device__ __forceinline__ uint32_t sa() const { return (uint32_t)S & 3u; }
     // block-aligned rows: dwords past the frame end in its last row (the row ends on a 64-B block)
@@ -1023,17 +871,16 @@ struct TileA {
     }
 };
 
-// kAl: BLOCK-ALIGNED rows -- each frame's rows are the 64-B blocks (half 128-B lines) that hold
-// it, the last one ending on the block boundary after the frame end (nd + ealign() dwords from
-// frame dword 0), so a row load never straddles a line; the end-anchored rows otherwise
-// (ending at the frame's dword-rounded end).
+// BLOCK-ALIGNED rows: each frame's rows are the 64-B blocks (half 128-B lines) that hold it, the
+// last one ending on the block boundary after the frame end (nd + ealign() dwords from frame
+// dword 0), so a row load never straddles a line.
 // The tile's masked-row count H and its capture flag (the last part of tile_geometry_a; the first
-// tile of the block-aligned kernel computes them after its first rows are issued, kDeferTail).
-template <bool kAl, int kCapBlocks = 3>
+// tile computes them after its first rows are issued, kDeferTail).
+template <int kCapBlocks = 3>
 __device__ __forceinline__ void tile_geometry_a_tail(TileA& T) {
     const int nd = T.nd();
-    const int ndb = (kAl && nd > 0) ? nd + T.ealign() : nd;
-    T.cap = __ballot(nd > 0 && min(T.r0f + kCapBlocks, T.P) > kRingA<kAl>) == 0;
+    const int ndb = nd > 0 ? nd + T.ealign() : nd;
+    T.cap = __ballot(nd > 0 && min(T.r0f + kCapBlocks, T.P) > kRingA) == 0;
     // Masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
     // dword before the frame. The group's lane 0 has the lowest rel: row r is lean for the
     // group once nd - 16 P + 16 r >= 2.
@@ -1041,7 +888,7 @@ __device__ __forceinline__ void tile_geometry_a_tail(TileA& T) {
     const int h = (nd > 0 && need > 0) ? (need + kRowDwords - 1) / kRowDwords : 0;
     T.H = min(group_max(h), T.P);
 }
-template <bool kAl, int kCapBlocks = 3, bool kDeferTail = false>
+template <int kCapBlocks = 3, bool kDeferTail = false>
 __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
                                               uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
                                               uint32_t fpt) {
@@ -1049,10 +896,10 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     T.S = S;
     T.ph = (uint32_t)((reinterpret_cast<uint64_t>(frames) >> 2) + T.sdw()) & 15u;
     const int nd = T.nd();
-    const int ndb = (kAl && nd > 0) ? nd + T.ealign() : nd;  // stream dwords up to the last row's end
-    const int rows = kAl ? (int)((T.ph + (uint32_t)ndb) >> 4) * (nd > 0) : (nd + kRowDwords - 1) / kRowDwords;
+    const int ndb = nd > 0 ? nd + T.ealign() : nd;  // stream dwords up to the last row's end
+    const int rows = (int)((T.ph + (uint32_t)ndb) >> 4) * (nd > 0);
     const int R = group_max(rows);
-    T.P = (R + kRingA<kAl> - 1) / kRingA<kAl> * kRingA<kAl>;
+    T.P = (R + kRingA - 1) / kRingA * kRingA;
     T.r0f = nd > 0 ? T.P - rows : (1 << 20);
     uint64_t ld_sdw = T.sdw();
     int ld_nd = ndb;
@@ -1072,15 +919,12 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     }
     T.gfb = reinterpret_cast<const uint32_t*>(frames + (ld_sdw << 2));
     T.rel0 = ld_nd - kRowDwords * T.P + 4 * (int)gl;
-    // Loads of rows that start before the frame are clamped to the frame's first chunk (its last
-    // chunk for frames under 4 dwords), so lanes idling through a tile's longest frame re-read
-    // one cached line instead of fetching the bytes that precede their frame; a chunk that
-    // straddles the frame start is loaded where it lies unless that is below frames[0].
-    // Block-aligned rows: lo = the frame dword where the frame's first block starts; a chunk
-    // below it reloads the lane's chunk of that block (a row inside a block that holds a frame
-    // byte never leaves that byte's page, so it needs no other clamp).
-    T.lo = kAl ? -(int)ld_ph : max(ld_sdw > (1u << 24) ? -(1 << 24) : -(int)ld_sdw, min(0, ld_nd - 4));
-    if (!kDeferTail) tile_geometry_a_tail<kAl, kCapBlocks>(T);
+    // Loads of rows that start before the frame's first block (lo = the frame dword where that
+    // block starts) reload the lane's chunk of that block, so lanes idling through a tile's longest
+    // frame re-read one cached line instead of fetching the bytes that precede their frame (a row
+    // inside a block that holds a frame byte never leaves that byte's page: no other clamp).
+    T.lo = -(int)ld_ph;
+    if (!kDeferTail) tile_geometry_a_tail<kCapBlocks>(T);
 }
 
 // Frame dword at which a masked row's chunk is loaded: where it lies, unless it starts
@@ -1104,7 +948,7 @@ __device__ __forceinline__ void prefetch_unit(const Unit& U, u32x4 (&pf)[kPrefet
 
 // The tables in place. Region A: thread t builds Z64[b][e] (b = t >> 8, e = t & 255) as the XOR
 // of the basis columns of e's set bits and stores its 8 copies (32 contiguous bytes). The plain
-// tables (FS_PLAIN_VALU): wave w builds the 1-KB pieces p = w, w + 16, w + 32 (< 40) of the
+// tables: wave w builds the 1-KB pieces p = w, w + 16, w + 32 (< 40) of the
 // 40 [4][256] tables the same way, lane l the entries 4l .. 4l + 3 (one ds_write_b128): no
 // LDS-DMA in the preamble's vector-memory burst, no wait for table pieces at the barrier.
 // The bases come in by scalar loads (lgkmcnt), all issued before one wait, so waiting for them
@@ -1121,7 +965,6 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
     const uint32_t e = t & 255u;
     const uint64_t sa = sgpr_addr(&tabs->z64_basis[b][0]);
     u32x8 basis;
-#if FS_PLAIN_VALU
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint32_t lane = t & 63u;
     const uint64_t s0 = sgpr_addr(&tabs->plain_basis[w][0]);
@@ -1133,9 +976,6 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
         "s_load_dwordx8 %2, %6, 0x0\n\ts_load_dwordx8 %3, %7, 0x0\n\ts_waitcnt lgkmcnt(0)"
         : "=&s"(basis), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
         : "s"(sa), "s"(s0), "s"(s1), "s"(s2));
-#else
-    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(basis) : "s"(sa));
-#endif
     uint32_t v = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
@@ -1145,7 +985,6 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
     u32x4* dst = reinterpret_cast<u32x4*>(lds + kLdsRegionA + e * 256u + 32u * b);
     dst[0] = u32x4{v, v, v, v};
     dst[1] = u32x4{v, v, v, v};
-#if FS_PLAIN_VALU
     auto piece = [&](const u32x8& pb, uint32_t p) {
         uint32_t x = 0;
 #pragma unroll
@@ -1156,7 +995,6 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
     piece(pb0, w);
     piece(pb1, w + 16u);
     if (w + 32u < 40u) piece(pb2, w + 32u);
-#endif
 }
 // LDS-DMA by inline asm: invisible to hipcc's vmcnt model (the builtin makes it drain later
 // LDS reads with vmcnt(0)); unknown VMEM ops only make the compiler's own counted waits
@@ -1183,20 +1021,6 @@ __device__ __forceinline__ uint32_t lds_base(const char* lds) {
     return (uint32_t)(uintptr_t)(lds_char*)lds;
 }
 
-// The plain tables: exactly kDmaPerWave 1-KB pieces per wave (surplus pieces re-copy the
-// last one with identical bytes).
-__device__ __forceinline__ void plain_dma(const FsTables* __restrict__ tabs, const char* lds, uint32_t wave,
-                                          uint32_t lane) {
-    const uint32_t lds0 = lds_base(lds);
-    const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-    for (uint32_t k = 0; k < (((FS_DIAG & 2) || FS_PLAIN_VALU) ? 0 : kDmaPerWave); ++k) {
-        const uint32_t c = min(w0 + k * kWavesPerBlock, kPlainChunks - 1u);
-        dma_x4(reinterpret_cast<const char*>(tabs) + (kPlainChunk0 + c) * 1024u + lane * 16u,
-               __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
-    }
-}
-
 // The tile's header slots: 8 dword DMAs; instruction i writes frame dword x = 4i + gl of
 // every group (lane-linear: LDS byte hw + 256 i + 4 lane). Sources are clamped to the
 // frame's last dword (never past it).
@@ -1212,7 +1036,6 @@ template <bool kX4, int kSlot = kHdrDwords, class TileT>
 __device__ __forceinline__ bool header_dma(const TileT& T, const uint8_t* __restrict__ frames, const char* lds,
                                            uint32_t hw, uint32_t gl, uint32_t lane) {
     static_assert(kSlot == 16 || kSlot == 32, "header slot: 16 or 32 dwords");
-    if (FS_DIAG & 1) return false;
     const uint32_t hdr0 = __builtin_amdgcn_readfirstlane(lds_base(lds) + hw);
     const int last = T.ndall() - 1;
     const bool own = T.len > 0u;
@@ -1271,18 +1094,13 @@ __device__ __forceinline__ void combine_piece(const char* lds, uint32_t gl, cons
     csum = cs;
 }
 
-// The one-pass kernel's LDS layouts. LayA1: one 16-wave workgroup per CU (region A built in
-// place, the plain tables by LDS-DMA, 3-block header slots). LayA2: two 8-wave workgroups per CU
-// (kA2* map above: region A and the plain tables in one 64-KB LDS-DMA image, 2-block header
-// slots; block-aligned RX kernels only -- the TX fill's long CRC shifts need Z768).
+// The one-pass kernel's LDS layout: one 16-wave workgroup per CU (region A and the plain tables
+// built in place), 3-block captured header slots per wave.
 struct LayA1 : LayoutA {
-    static constexpr int kWaves = kWavesPerBlock;
-    static constexpr bool kL2 = false;
     static constexpr uint32_t kRegion = kLdsRegionA;
     static constexpr uint32_t kHdr = kLdsHdr;
     static constexpr uint32_t kCapStride = 3072;
     static constexpr int kCapBlocks = 3;
-    static constexpr int kSlotAl = FS_HDR_AL;
     // the combine's shifts Z_(4c), c = 1..3, and Z_(16a), a = 1..3
     __device__ static __forceinline__ uint32_t z4c(const char* lds, uint32_t v, uint32_t c) {
         return zplain(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
@@ -1291,102 +1109,6 @@ struct LayA1 : LayoutA {
         return zplain(lds, v, a == 1u ? kLdsZ16 : a == 2u ? kLdsZ32 : kLdsZ48);
     }
 };
-struct LayA2 {
-    static constexpr int kWaves = kA2Waves;
-    static constexpr bool kL2 = true;
-    static constexpr uint32_t kRegion = 0;
-    static constexpr uint32_t kHdr = kA2Hdr;
-    static constexpr uint32_t kCapStride = kA2HdrStride;
-    static constexpr int kCapBlocks = 2;
-    // the captured slot holds frame dwords [0, 32 - ph) with ph <= 15: the parse treats it as a
-    // 16-dword slot (frame_dw_t / slot_sum read what lies past it from global memory)
-    static constexpr int kSlotAl = 16;
-    // plain table t (kA2Tables: Z4 Z8 Z12 Z16 Z32 Z48 Z2 Z1) in region A's upper half, swizzled
-    __device__ static __forceinline__ uint32_t zt(const char* lds, uint32_t v, uint32_t t) {
-        uint32_t r = 0u;
-#pragma unroll
-        for (uint32_t b = 0; b < 4; ++b) {
-            const uint32_t e = (v >> (8u * b)) & 0xffu;
-            r ^= lds32(lds, (e << 8) + 128u + (((4u * t + b) ^ (e & 31u)) << 2));
-        }
-        return r;
-    }
-    __device__ static __forceinline__ uint32_t z4c(const char* lds, uint32_t v, uint32_t c) { return zt(lds, v, c - 1u); }
-    __device__ static __forceinline__ uint32_t z16a(const char* lds, uint32_t v, uint32_t a) { return zt(lds, v, a + 2u); }
-    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
-        if (t == 1u) v = zt(lds, v, 6u);  // Z3 = Z1 Z2
-        return zt(lds, v, t == 0u ? 0u : t == 2u ? 6u : 7u);
-    }
-    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) {
-        return lds32(lds, (i << 8) + 128u + ((28u ^ (i & 31u)) << 2));
-    }
-};
-
-// LayA2's tables built in place by VALU (FS_A2_VALU), in FsTables::region_a's layout: thread t
-// builds Z64[b][e] for e = t & 255 and b = 2 (t >> 8), 2 (t >> 8) + 1 (8 copies each); wave w builds
-// the upper-half plain pieces q = w + 8k (k = 0..3), lane l the entries 4l .. 4l + 3 of each. All
-// six bases by scalar loads issued before one wait (no vector-memory op at all).
-__device__ __forceinline__ void a2_tables_build(const FsTables* __restrict__ tabs, char* lds, uint32_t wave,
-                                                uint32_t lane) {
-    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-    const uint32_t t = threadIdx.x;
-    const uint32_t h = __builtin_amdgcn_readfirstlane(t >> 8);
-    const uint32_t e = t & 255u;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(wave);
-    const uint64_t a0 = sgpr_addr(&tabs->z64_basis[2u * h][0]), a1 = sgpr_addr(&tabs->z64_basis[2u * h + 1u][0]);
-    const uint64_t q0 = sgpr_addr(&tabs->a2_basis[w][0]), q1 = sgpr_addr(&tabs->a2_basis[w + 8u][0]);
-    const uint64_t q2 = sgpr_addr(&tabs->a2_basis[w + 16u][0]), q3 = sgpr_addr(&tabs->a2_basis[w + 24u][0]);
-    u32x8 z0, z1, p0, p1, p2, p3;
-    asm volatile(
-        "s_load_dwordx8 %0, %6, 0x0\n\ts_load_dwordx8 %1, %7, 0x0\n\ts_load_dwordx8 %2, %8, 0x0\n\t"
-        "s_load_dwordx8 %3, %9, 0x0\n\ts_load_dwordx8 %4, %10, 0x0\n\ts_load_dwordx8 %5, %11, 0x0\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&s"(z0), "=&s"(z1), "=&s"(p0), "=&s"(p1), "=&s"(p2), "=&s"(p3)
-        : "s"(a0), "s"(a1), "s"(q0), "s"(q1), "s"(q2), "s"(q3));
-    uint32_t v0 = 0, v1 = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t m = 0u - ((e >> j) & 1u);
-        v0 ^= z0[j] & m;
-        v1 ^= z1[j] & m;
-    }
-    u32x4* dst = reinterpret_cast<u32x4*>(lds + e * 256u + 64u * h);
-    dst[0] = u32x4{v0, v0, v0, v0};
-    dst[1] = u32x4{v0, v0, v0, v0};
-    dst[2] = u32x4{v1, v1, v1, v1};
-    dst[3] = u32x4{v1, v1, v1, v1};
-    auto piece = [&](const u32x8& pb, uint32_t q) {
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
-        const uint32_t x1 = x ^ pb[0];
-        const uint32_t xv[4] = {x, x1, x ^ pb[1], x1 ^ pb[1]};
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) {
-            const uint32_t en = 4u * lane + i;
-            *reinterpret_cast<uint32_t*>(lds + (en << 8) + 128u + ((q ^ (en & 31u)) << 2)) = xv[i];
-        }
-    };
-    piece(p0, w);
-    piece(p1, w + 8u);
-    piece(p2, w + 16u);
-    piece(p3, w + 24u);
-}
-
-// LayA2's tables: region A's 64 KB as FsTables holds it (Z64's copies and the plain tables), 8
-// pieces of 1 KB per wave. (Building the Z64 half in place and copying only the plain tables'
-// 32 KB, lane-masked, measured 2-3% slower: the basis loads wait behind the DMAs.)
-__device__ __forceinline__ void a2_tables_dma(const FsTables* __restrict__ tabs, const char* lds, uint32_t wave,
-                                              uint32_t lane) {
-    const uint32_t lds0 = lds_base(lds);
-    const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-    for (uint32_t k = 0; k < ((FS_DIAG & 2) ? 0u : 65536u / 1024u / kA2Waves); ++k) {
-        const uint32_t c = w0 + k * kA2Waves;
-        dma_x4(reinterpret_cast<const char*>(tabs->region_a) + c * 1024u + lane * 16u,
-               __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
-    }
-}
 
 // `report` = the host-mapped report word's address in bits 0..47, the launch id in bits 48..63
 // (one kernel argument, loaded where it is used: nothing of it stays live through the tile loop).
@@ -1395,71 +1117,45 @@ __device__ __forceinline__ void post_report(uint64_t report) {
     *reinterpret_cast<uint32_t*>(report & 0xFFFFFFFFFFFFull) = (uint32_t)(report >> 48);
 }
 
-// The kernel for batches of similar lengths: every tile in mode A (one pass). It reports in
-// `report` whether any tile would have run better in mode B, so that the host launches
-// digest_kernel_ab next time (launch_digest).
-// The wave's first tile (later tiles: + all waves). Every map is a bijection on [0, nwaves).
-template <int kW = kWavesPerBlock>
-__device__ __forceinline__ uint32_t first_tile(uint32_t wave) {
-    if (FS_TILE_MAP == 1) return wave * gridDim.x + blockIdx.x;
-    if (FS_TILE_MAP == 2 && (gridDim.x & 7u) == 0u) {  // workgroup b runs on XCD b % 8
-        const uint32_t per = gridDim.x >> 3;
-        return ((blockIdx.x & 7u) * per + (blockIdx.x >> 3)) * kW + wave;
-    }
-    return blockIdx.x * kW + wave;
-}
+// The wave's first tile (later tiles: + all waves): wave-major, so a workgroup's waves read tiles
+// spread over the batch and neighbouring workgroups (on different XCDs) neighbouring tiles.
+__device__ __forceinline__ uint32_t first_tile(uint32_t wave) { return wave * gridDim.x + blockIdx.x; }
 
-template <uint32_t kOps, bool kAl, class Lay = LayA1>
-__global__ void __launch_bounds__(Lay::kWaves * kWave, 1)
+// The kernel for batches of similar lengths: every tile in one pass over block-aligned rows. It
+// reports in `report` whether any tile would have run better in mode B, so that the host launches
+// digest_kernel_ab next time (launch_digest).
+template <uint32_t kOps>
+__global__ void __launch_bounds__(kThreads, 1)
 digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
                 const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
                 uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx, uint32_t fpt) {
-    static_assert(!Lay::kL2 || (kAl && FS_HDR_CAPTURE && kOps != kOpsTx), "LayA2: block-aligned RX kernels with header capture");
-    char* lds = lds_image<Lay::kL2>();
-    constexpr int kPfA = kRingA<kAl>;
-    // header slot dwords (FS_HDR_AL = 16 with block-aligned rows: one dwordx4 DMA per wave, the
-    // parse reading the rare bytes past the slot from global memory; measured within noise of 32)
-    constexpr int kSlotA = kAl ? Lay::kSlotAl : kHdrDwords;
+    using Lay = LayA1;
+    char* lds = g_lds;
+    constexpr int kPfA = kRingA;
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t grp = lane >> 2;   // frame slot of this lane's group
     const uint32_t gl = lane & 3u;    // lane within the group
-    const uint32_t gwave = first_tile<Lay::kWaves>(wave);
-    const uint32_t nwaves = gridDim.x * Lay::kWaves;
+    const uint32_t gwave = first_tile(wave);
+    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
     // fpt: frames per tile (16, or 8 / 4 for batches too small to give every wave a tile;
     // the other groups stay empty)
     fpt = __builtin_amdgcn_readfirstlane(fpt);
     const uint32_t ntiles = (n + fpt - 1) / fpt;
-    // Header slots captured from the rows (block-aligned rows, FS_HDR_CAPTURE): the first block
-    // of rows holds every frame's first 3 blocks (checked per tile: T.cap), and each of those
-    // rows is written to the slot as it is consumed -- cell 4k + gl of the slot holds the lane's
-    // 16 B of the frame's block k, so slot dword s is frame dword s - ph (the parse's `xo`).
-    // No header DMA: its 2 KB per wave were 0.5 us of the preamble's vector-memory burst. 3 KB
-    // per wave (12 cells), overlapping the wave scratch the one-pass kernel leaves unused.
-    constexpr bool kCapture = kAl && FS_HDR_CAPTURE;
-    // the first tile's masked-row count and capture flag after its first rows are issued
-    constexpr bool kEarlyRows = kCapture && FS_EARLY_ROWS;
-    // the tables barrier right after the in-place table build (FS_TABLES_BARRIER; only when no table
-    // comes by LDS-DMA): each wave then issues and consumes its first rows on its own descriptors
-    constexpr bool kTablesBarrier =
-        FS_TABLES_BARRIER && !FS_EARLY_BARRIER && FS_PLAIN_VALU && (!Lay::kL2 || FS_A2_VALU) && !(FS_DIAG & 2);
-    constexpr uint32_t kHwStride = kCapture ? Lay::kCapStride : kHdrWaveBytes;
-    static_assert(Lay::kHdr + Lay::kWaves * Lay::kCapStride <= (Lay::kL2 ? kA2Bytes : kLdsBytes), "captured header slots fit");
+    // Header slots captured from the rows: the first block of rows holds every frame's first 3
+    // blocks (checked per tile: T.cap), and each of those rows is written to the slot as it is
+    // consumed -- cell 4k + gl of the slot holds the lane's 16 B of the frame's block k, so slot
+    // dword s is frame dword s - ph (the parse's `xo`). 3 KB per wave (12 cells), overlapping the
+    // wave scratch this kernel leaves unused.
+    static_assert(Lay::kHdr + kWavesPerBlock * Lay::kCapStride <= kLdsBytes, "captured header slots fit");
     static_assert(4u * Lay::kCapBlocks * 256u <= Lay::kCapStride, "a wave's captured cells fit its stride");
-    const uint32_t hw = Lay::kHdr + wave * kHwStride;  // this wave's header slots
-    // where the parse is parked until the finish: the header slot itself, or with chained tiles
-    // (the next tile's header DMA lands before this tile's finish) the wave's scratch area,
-    // which the one-pass kernel does not otherwise use
-    constexpr bool kChain = kAl && FS_CHAIN && !kCapture;
-    const uint32_t pk = kChain ? kLdsWave + wave * kWaveScratchBytes : hw;
-    // where a masked row's chunk is loaded (block-aligned rows: where it lies, or wholly before
-    // the frame's first block, the lane's chunk of that block)
-    auto lpos = [&](int rel, int lo) -> int { return kAl ? (rel >= lo ? rel : lo + 4 * (int)gl) : load_pos(rel, lo); };
-    // the tile's header slots: by LDS-DMA, or (capture mode) from the first block of rows, or for
-    // a tile whose frames start too late for that, by plain loads here (rare: mixed lengths)
-    auto tile_header = [&](const TileA& Tt) -> bool {
-        if (!kCapture) return header_dma<true, kSlotA>(Tt, frames, lds, hw, gl, lane);
+    const uint32_t hw = Lay::kHdr + wave * Lay::kCapStride;  // this wave's header slots (and parked parse)
+    // where a masked row's chunk is loaded: where it lies, or wholly before the frame's first
+    // block, the lane's chunk of that block
+    auto lpos = [&](int rel, int lo) -> int { return rel >= lo ? rel : lo + 4 * (int)gl; };
+    // the slots of a tile whose frames start too late for the capture: plain loads (rare: mixed lengths)
+    auto tile_header = [&](const TileA& Tt) {
         if (!Tt.cap) {
             const int rows = Tt.P - Tt.r0f;
             const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + (Tt.sdw() << 2));
@@ -1471,7 +1167,6 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 }
             }
         }
-        return false;
     };
 
     LaneKeys keys;
@@ -1487,10 +1182,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         }
     }
 
-    // Preamble: the first tile's descriptors (the first memory ops, one round trip) while
-    // region A is built in place by VALU; geometry; the plain tables' LDS-DMA (36 KB, L2
-    // hits); the header DMA; the row prefetch; one barrier once this wave's table pieces
-    // have landed.
+    // Preamble: the first tile's descriptors (the first memory ops, one round trip) while the
+    // tables are built in place by VALU; geometry; the first rows; the masked-row count and the
+    // capture flag; one barrier once this wave's table stores are done.
     uint32_t tile = gwave;
     FS_RTSTAMP(5);
     FS_STAMP(0);
@@ -1500,89 +1194,33 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     {
         uint64_t S;
         uint32_t len;
-        if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(3);  // the preamble outranks other waves' row loops
         tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
-        if constexpr (Lay::kL2) {
-            if (FS_A2_VALU) a2_tables_build(tabs, lds, wave, lane);
-            else a2_tables_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
-        } else {
-            if (FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
-            build_region_a(tabs, lds);
-        }
-        if (kTablesBarrier) {
-            // every table is built in place (no DMA): one barrier on this wave's LDS stores, while its
-            // descriptors are still in flight -- after it no wave waits for another's descriptors
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
-            __builtin_amdgcn_s_barrier();
-        }
+        build_region_a(tabs, lds);
         FS_STAMP(7);
         descriptors_ready<kOps>(S, len);
         FS_STAMP(8);
-        if (FS_EARLY_BARRIER) {
-            // the tables are ready here: the descriptors' vmcnt(0) also retired the table pieces
-            // (issued before them), lgkmcnt(0) this wave's region-A stores; the geometry and the
-            // first rows follow the barrier, so no wave waits for another's row issue
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_s_barrier();
-        }
         T.P = 0;
-        if (first) {
-            tile_geometry_a<kAl, Lay::kCapBlocks, kEarlyRows>(T, tile, grp, gl, n, S, len, frames, fpt);
-            FS_STAMP(11);
-            // (block-aligned rows with header capture: the report after the first rows' issue, below)
-            if (!FS_LATE_REPORT && !(kCapture && FS_REPORT_AFTER_ROWS) && report && mode_b_worthy(T.nd()) && lane == 0u)
-                post_report(report);
-            FS_STAMP(12);
-        }
+        if (first) tile_geometry_a<Lay::kCapBlocks, true>(T, tile, grp, gl, n, S, len, frames, fpt);
+        FS_STAMP(11);
+        FS_STAMP(12);
     }
-    if (!Lay::kL2 && !FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);
-    bool x4 = false;
-    auto first_rows = [&]() {
-        if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
+    if (first && T.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-            for (int i = 0; i < kPfA; ++i) {
-                const int rel = T.rel0 + kRowDwords * i;
-                // (block-aligned rows: lpos is the identity on lean rows, so H is not needed here)
-                pf[i] = load_row(T.gfb, (kEarlyRows || i < T.H) ? lpos(rel, T.lo) : rel);
-            }
-        }
-    };
-    // (FS_ROWS_FIRST: the first rows before the header DMA -- still older than the first
-    // block's refills, which is all the parse's vmcnt(kPfA) needs; measured within noise)
-    if (FS_ROWS_FIRST || kCapture) first_rows();
-    if (kEarlyRows && first) tile_geometry_a_tail<kAl, Lay::kCapBlocks>(T);
-    if (kCapture && FS_REPORT_AFTER_ROWS && !FS_LATE_REPORT && first && report && mode_b_worthy(T.nd()) && lane == 0u)
-        post_report(report);
-    if (first) x4 = tile_header(T);
+        for (int i = 0; i < kPfA; ++i) pf[i] = load_row(T.gfb, lpos(T.rel0 + kRowDwords * i, T.lo));
+    }
+    if (first) tile_geometry_a_tail<Lay::kCapBlocks>(T);
+    if (first && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+    if (first) tile_header(T);
     FS_STAMP(13);
-    if (!FS_ROWS_FIRST && !kCapture) first_rows();
     FS_STAMP(9);
-    if (FS_EARLY_BARRIER || kTablesBarrier) {
-        // (the tables were ready at the early barrier)
-    } else if (kCapture) {  // no header DMA: the table pieces are older than the rows
-        if (first && T.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
-        else __builtin_amdgcn_s_waitcnt(0x0070);
-    } else {
-        tables_landed<kPfA, kSlotA>(first, T.P > 0, x4);
-    }
+    // the tables are this wave's own LDS stores: only the rows stay in flight
+    if (first && T.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
+    else __builtin_amdgcn_s_waitcnt(0x0070);
     FS_STAMP(10);
-    if (!FS_EARLY_BARRIER && !kTablesBarrier)
-        __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
-    if (FS_PRE_PRIO) __builtin_amdgcn_s_setprio(0);
-    if (FS_AGE_PRIO == 1) {  // the SIMD's younger waves (wave >> 2: its 4 waves in launch order) outrank the older
-        const uint32_t w = __builtin_amdgcn_readfirstlane(wave) >> 2;
-        if (w == 3u) __builtin_amdgcn_s_setprio(3);
-        else if (w == 2u) __builtin_amdgcn_s_setprio(2);
-        else if (w == 1u) __builtin_amdgcn_s_setprio(1);
-    } else if (FS_AGE_PRIO == 2) {  // two levels: the SIMD's younger half (waves 8..15) outranks the older
-        if ((__builtin_amdgcn_readfirstlane(wave) >> 3) != 0u) __builtin_amdgcn_s_setprio(1);
-    } else if (FS_AGE_PRIO == 3) {  // (experiment) the SIMD's youngest wave (12..15) only
-        if ((__builtin_amdgcn_readfirstlane(wave) >> 2) == 3u) __builtin_amdgcn_s_setprio(1);
-    } else if (FS_AGE_PRIO == 4) {  // (experiment) three levels: 0, 1, 1, 2
-        const uint32_t w = __builtin_amdgcn_readfirstlane(wave) >> 2;
-        if (w == 3u) __builtin_amdgcn_s_setprio(2);
-        else if (w != 0u) __builtin_amdgcn_s_setprio(1);
-    }
+    __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    // two-level age priority: the SIMD's younger half (waves 8..15) outranks the older (round 2:
+    // -0.35..-0.55 us per launch)
+    if ((__builtin_amdgcn_readfirstlane(wave) >> 3) != 0u) __builtin_amdgcn_s_setprio(1);
     FS_STAMP(1);
 
     while (tile < ntiles) {
@@ -1592,36 +1230,17 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         const bool fvalid = grp < fpt && tile * fpt + grp < n;
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
         const int Rc = T.P - kPfA;  // first row of the last block
-        // Chained tiles (block-aligned kernel): the next tile's descriptors are loaded right after
-        // this tile's parse, its geometry is set up before the last block, and the last block
-        // refills the ring with the next tile's first rows, so the ring never drains between a
-        // wave's tiles. It needs a block of refills between the parse and the last block (the
-        // descriptors must be older than the ring's loads there): tiles of 3+ blocks.
-        const uint32_t tnext = tile + nwaves;
-        const bool chain = kChain && tnext < ntiles && Rc >= 2 * kPfA;
-        uint64_t Sn = 0;
-        uint32_t lenn = 0;
-        TileA Tn;
-        Tn.P = 0;
 
-        // ---- header parse: after the first block of rows, while the ring's loads are in flight.
-        // The header DMA was issued before the tile's rows; vmcnt(kPfA) retires it once the
-        // first block's refills are the only younger loads.
-        auto parse = [&](bool refilled) {
-            if (!kCapture) {  // the DMA'd slot (captured slots are this wave's own LDS writes)
-                if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
-                else __builtin_amdgcn_s_waitcnt(0x0070);
-            }
-            if (!(FS_DIAG & 16))  // (diagnostic builds: 16 skips the parse)
-                parse_tile<kOps, kSlotA, Lay::kL2>(hw, grp, gl, T.sa(), T.len, mtu, reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)),
-                           parser, pk, kCapture ? T.ph : 0u);
-            if (FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
-            if (chain) tile_descriptors(tnext, grp, n, offsets, lengths, Sn, lenn, fpt);
+        // ---- header parse: after the first block of rows (the captured slot is this wave's own
+        // LDS writes), while the ring's loads are in flight
+        auto parse = [&]() {
+            parse_tile<kOps, kHdrDwords>(hw, grp, gl, T.sa(), T.len, mtu,
+                                         reinterpret_cast<const uint32_t*>(frames + (T.sdw() << 2)), parser, hw, T.ph);
         };
         auto prio = [&](int r0) {
-            // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
-            // a wave with more rows left gets a higher priority.
-            if (FS_PRIO && T.P > FS_PRIO_MIN) {  // long tiles only (C2-size tiles run faster without)
+            // Self-balancing issue priority for long tiles (C2-size tiles run faster without): the
+            // SIMD arbiter favours the oldest wave, a wave with more rows left gets a higher priority.
+            if (T.P > kPrioMinRows) {
                 const int left4 = (4 * (T.P - r0)) / max(T.P, 1);  // 4 .. 1
                 if (left4 >= 4) __builtin_amdgcn_s_setprio(3);
                 else if (left4 == 3) __builtin_amdgcn_s_setprio(2);
@@ -1629,12 +1248,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 else __builtin_amdgcn_s_setprio(0);
             }
         };
-        // general block: rows below H take the masked path (scalar branch per row); refills
-        // of rows below H are clamped. Refill kind: 0 none (the tile's last block), 1 this
-        // tile's rows kPfA ahead, 2 the next tile's first rows (the last block, chained).
+        // general block: rows below H take the masked path (scalar branch per row); refills of
+        // rows below H are clamped. kRefill: this tile's rows kPfA ahead (false: the last block).
         auto block = [&](int r0, auto refill_tag) {
-            constexpr int kKind = decltype(refill_tag)::value;
-            constexpr bool kRefill = kKind == 1;
+            constexpr bool kRefill = decltype(refill_tag)::value;
             prio(r0);
 #pragma unroll
             for (int i = 0; i < kPfA; ++i) {
@@ -1642,119 +1259,75 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 const int rel = T.rel0 + kRowDwords * r;
                 // consume the ring slot, then refill the SAME registers: no copy of an
                 // in-flight load, so the compiler keeps kPfA-1 loads outstanding
-                const bool masked = r < T.H;
-                if (kAl && masked) masked_row_al<Lay::kRegion>(lds, keys, pf[i], rel, T.nd(), T.sa(), T.tail_mask(), A, cs);
-                else if (masked) masked_row<Lay::kRegion>(lds, keys, pf[i], rel, load_pos(rel, T.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
-                else if (kAl && !kRefill && i == kPfA - 1) tail_row_al<Lay::kRegion>(lds, keys, pf[i], rel, T.nd(), T.tail_mask(), A, cs);
+                if (r < T.H) masked_row_al<Lay::kRegion>(lds, keys, pf[i], rel, T.nd(), T.sa(), T.tail_mask(), A, cs);
+                else if (!kRefill && i == kPfA - 1) tail_row_al<Lay::kRegion>(lds, keys, pf[i], rel, T.nd(), T.tail_mask(), A, cs);
                 else lean_row<Lay::kRegion>(lds, keys, pf[i], A, cs);
-                if (kCapture && r0 == 0 && T.cap) {  // the frame's first blocks into the header slot
+                if (r0 == 0 && T.cap) {  // the frame's first blocks into the header slot
                     const uint32_t k = (uint32_t)(i - T.r0f);
                     if (k < (uint32_t)Lay::kCapBlocks) *reinterpret_cast<u32x4*>(lds + hw + (4u * k + gl) * 256u + grp * 16u) = pf[i];
                 }
                 if (kRefill) {
                     const int rn = rel + kRowDwords * kPfA;
                     pf[i] = load_row(T.gfb, r + kPfA < T.H ? lpos(rn, T.lo) : rn);
-                } else if (kKind == 2) {
-                    const int rn = Tn.rel0 + kRowDwords * i;
-                    pf[i] = load_row(Tn.gfb, i < Tn.H ? lpos(rn, Tn.lo) : rn);
                 }
             }
         };
         // lean block: every row lean for every lane; the refills lie inside the frame, so they
         // need no clamp: one pointer per block, immediate row offsets
         auto lean_block = [&](int r0, auto refill_tag) {
-            constexpr int kKind = decltype(refill_tag)::value;
-            constexpr bool kRefill = kKind == 1;
+            constexpr bool kRefill = decltype(refill_tag)::value;
             prio(r0);
             const uint32_t* pb = T.gfb + (T.rel0 + kRowDwords * (r0 + kPfA));
 #pragma unroll
             for (int i = 0; i < kPfA; ++i) {
-                if (kAl && !kRefill && i == kPfA - 1)
+                if (!kRefill && i == kPfA - 1)
                     tail_row_al<Lay::kRegion>(lds, keys, pf[i], T.rel0 + kRowDwords * (r0 + i), T.nd(), T.tail_mask(), A, cs);
                 else lean_row<Lay::kRegion>(lds, keys, pf[i], A, cs);
-                if (kRefill) {
-                    pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
-                } else if (kKind == 2) {
-                    const int rn = Tn.rel0 + kRowDwords * i;
-                    pf[i] = load_row(Tn.gfb, i < Tn.H ? lpos(rn, Tn.lo) : rn);
-                }
+                if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
                 // keep consume/refill interleaved per row: unfenced, the scheduler sinks all
                 // refills to the block end behind a vmcnt(0), draining the ring every block
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
-        using Yes = std::integral_constant<int, 1>;
-        using No = std::integral_constant<int, 0>;
-        using Next = std::integral_constant<int, 2>;
+        using Yes = std::true_type;
+        using No = std::false_type;
         if (T.P > 0) {
             // [first block] parse [head blocks: general] [body: lean] [last block: no refill]
             if (Rc > 0) {
                 if (T.H > 0) block(0, Yes());
                 else lean_block(0, Yes());
-                parse(true);
+                parse();
                 int r0 = kPfA;
                 for (; r0 < Rc && r0 < T.H; r0 += kPfA) block(r0, Yes());
                 for (; r0 < Rc; r0 += kPfA) lean_block(r0, Yes());
-                if (chain) {
-                    // the next tile's descriptors are older than the ring's kPfA loads
-                    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(Sn), "+v"(lenn) : "n"(kPfA));
-                    if (kOps == kOpsFcs) lenn = lenn >= 4u ? lenn - 4u : 0u;
-                    tile_geometry_a<kAl, Lay::kCapBlocks>(Tn, tnext, grp, gl, n, Sn, lenn, frames, fpt);
-                    if (report && mode_b_worthy(Tn.nd()) && lane == 0u) post_report(report);
-                    if (Rc < T.H) block(Rc, Next());
-                    else lean_block(Rc, Next());
-                    // this tile's header slot is free (its parse is parked in the wave scratch)
-                    header_dma<true, kSlotA>(Tn, frames, lds, hw, gl, lane);
-                } else if (Rc < T.H) {
-                    block(Rc, No());
-                } else {
-                    lean_block(Rc, No());
-                }
+                if (Rc < T.H) block(Rc, No());
+                else lean_block(Rc, No());
             } else {
                 if (T.H > 0) block(0, No());
                 else lean_block(0, No());
-                parse(false);
+                parse();
             }
         } else {
-            parse(false);  // no rows (every frame of the tile under 4 bytes): rejected by length
+            parse();  // no rows (every frame of the tile under 4 bytes): rejected by length
         }
-        if (FS_FIN_PRIO) __builtin_amdgcn_s_setprio(3);  // (experiment) the combine and finish outrank row loops
         FS_STAMP(2);
 
-        // ---- combine the 16 streams of each frame: C = Z_(4-t)( xor_l Z_16(3-l)( U_l ) ),
-        //      U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3   (3 dependent LDS round trips).
-        // The last row was lean (unless every row was masked): its last dword -- lane 3's
-        // 4th -- still holds the up to 3 bytes past the frame end. Their CRC contribution is
-        // that junk itself (the last dword enters the combine unshifted) and their sum is
-        // sad16 of it: remove both.
-        // the parked parse, read by every lane now: its LDS round trip overlaps the combine's
-        const Parsed P = unpark_parsed<kOps>(lds, pk, grp);
-        uint32_t Y;
-        if (kAl) {
-            // block-aligned rows: stream j of lane gl (row position 4 gl + j) is shifted by its
-            // distance in dwords to the frame's last dword, at position q = 15 - ealign() of the
-            // last row: (q - 4 gl - j) mod 16 (the streams past q skipped the last row), as
-            // Z_(16 a) Z_(4 c) with s = 4 a + c
-            const uint32_t kq = (uint32_t)(15 - T.ealign() - 4 * (int)gl);
-            Y = 0u;
+        // ---- combine the 16 streams of each frame. Stream j of lane gl (row position 4 gl + j)
+        // is shifted by its distance in dwords to the frame's last dword, at position
+        // q = 15 - ealign() of the last row: (q - 4 gl - j) mod 16 (the streams past q skipped the
+        // last row), as Z_(16 a) Z_(4 c) with s = 4 a + c; then xor over the group's 4 lanes.
+        // The parked parse, read by every lane now: its LDS round trip overlaps the combine's.
+        const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
+        const uint32_t kq = (uint32_t)(15 - T.ealign() - 4 * (int)gl);
+        uint32_t Y = 0u;
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t sh = (kq - j) & 15u, c = sh & 3u, a4 = sh >> 2;
-                uint32_t v = A[j];
-                const uint32_t v1 = Lay::z4c(lds, v, c);
-                v = c ? v1 : v;
-                const uint32_t v2 = Lay::z16a(lds, v, a4);
-                Y ^= a4 ? v2 : v;
-            }
-        } else {
-            uint32_t junk = 0u;
-            if (T.P > 0 && T.H < T.P && gl == 3u && T.nd() > 0) junk = pf[kPfA - 1].w & ~T.tail_mask();
-            const uint32_t U =
-                zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3] ^ junk;
-            cs -= sad16(junk, 0u);
-            const uint32_t ybase = (gl == 0u) ? kLdsZ48 : (gl == 1u) ? kLdsZ32 : kLdsZ16;
-            Y = zplain(lds, U, ybase);
-            if (gl == 3u) Y = U;
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t sh = (kq - j) & 15u, c = sh & 3u, a4 = sh >> 2;
+            uint32_t v = A[j];
+            const uint32_t v1 = Lay::z4c(lds, v, c);
+            v = c ? v1 : v;
+            const uint32_t v2 = Lay::z16a(lds, v, a4);
+            Y ^= a4 ? v2 : v;
         }
         Y ^= dpp_quad<kQuadXor1>(Y);
         Y ^= dpp_quad<kQuadXor2>(Y);
@@ -1765,24 +1338,19 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         cs += dpp_quad<kQuadXor2>(cs);
         FS_STAMP(3);
         // ---- the group's lane 0: finish and store (its frame's parse comes back from LDS).
-        if ((FS_DIAG & 32) && parser)  // (diagnostic builds: 32 stores the raw combine, no finish)
-            out[tile * fpt + grp] = uint2{Y, cs};
-        else if (parser)
-            finish_frame<kOps, Lay>(lds, P, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths,
-                               tile * fpt + grp, out, status, tx);
+        if (parser)
+            finish_frame<kOps, Lay>(lds, P, T.S, T.len, T.te(), Y, cs, frames, wframes, lengths, tile * fpt + grp, out,
+                                    status, tx);
         FS_STAMP(4);
         FS_RTSTAMP(6);
-        tile = tnext;
-        if (chain) {
-            T = Tn;  // its first rows are in the ring, its header DMA issued
-        } else if (tile < ntiles) {  // next tile: descriptors, geometry, header DMA, row prefetch
+        tile += nwaves;
+        if (tile < ntiles) {  // next tile: descriptors, geometry, row prefetch, header slots
             uint64_t S;
             uint32_t len;
             tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
             descriptors_ready<kOps>(S, len);
-            tile_geometry_a<kAl, Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
-            if (!FS_LATE_REPORT && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
-            if (!kCapture) tile_header(T);
+            tile_geometry_a<Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
+            if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             if (T.P > 0) {
 #pragma unroll
                 for (int i = 0; i < kPfA; ++i) {
@@ -1790,7 +1358,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                     pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
                 }
             }
-            if (kCapture) tile_header(T);
+            tile_header(T);
         }
     }
 }
@@ -1832,10 +1400,9 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         }
     }
 
-    // Preamble: the first tile's descriptors (the first memory ops, one round trip) while
-    // region A is built in place by VALU; geometry; the plain tables' LDS-DMA (40 KB, L2
-    // hits); the header DMA; the row prefetch; one barrier once this wave's table pieces
-    // have landed.
+    // Preamble: the first tile's descriptors (the first memory ops, one round trip) while the
+    // tables are built in place by VALU; geometry; the row prefetch; the header DMA; one barrier
+    // once the header DMA has landed.
     uint32_t tile = gwave;
     FS_RTSTAMP(5);
     FS_STAMP(0);
@@ -1847,24 +1414,21 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         uint64_t S;
         uint32_t len;
         tile_descriptors(tile, grp0, n, offsets, lengths, S, len, fpt);
-        if (FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);  // lands before descriptors_ready's vmcnt(0)
         build_region_a(tabs, lds);
         descriptors_ready<kOps>(S, len);
         U.P = 0;
         if (first) tile_geometry(T, U, tile, grp0, gl0, n, S, len, frames, lds, ws, fpt);
     }
-    if (!FS_EARLY_TABLES) plain_dma(tabs, lds, wave, lane);
     bool x4 = false;
-    // FS_AB_ROWS_FIRST: the first rows ahead of the header DMA (still older than the first block's
-    // refills, which is all the parse's vmcnt(kPrefetch) needs)
-    if (FS_AB_ROWS_FIRST && first) prefetch_unit(U, pf);
+    // the first rows ahead of the header DMA (still older than the first block's refills, which
+    // is all the parse's vmcnt(kPrefetch) needs)
+    if (first) prefetch_unit(U, pf);
     if (first) x4 = header_dma<false>(T, frames, lds, hw, gl0, lane);
-    if (!FS_AB_ROWS_FIRST && first) prefetch_unit(U, pf);
     FS_STAMP(9);
     tables_landed<kPrefetch>(first, U.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
-    if (FS_AGE_PRIO_AB == 2 && (wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // the SIMD's younger half first
+    if ((wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // two-level age priority: the SIMD's younger half first
     FS_STAMP(1);
 
     while (tile < ntiles) {
@@ -1877,7 +1441,6 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         const bool fvalid = grp < fpt && tile * fpt + grp < n;
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
         const int npass = T.npass;
-        const int total_rows = U.P + kPieceRows * (npass - 1);
         if (npass > 1 && lane == 0u && report) post_report(report);  // this launch met a mixed tile
 
         // ---- header parse: after the first block of rows, while the ring's loads are in flight.
@@ -1895,23 +1458,10 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             asm volatile("" : "+v"(grp), "+v"(gl));
             uint32_t A[4] = {0u, 0u, 0u, 0u};
             uint32_t cs = 0u;
-            const int done0 = pass == 0 ? 0 : U.P == 0 ? 0 : (total_rows - kPieceRows * (npass - pass));
-            auto prio = [&](int r0) {
-                // Self-balancing issue priority: the SIMD arbiter favours the oldest wave,
-                // a wave with more rows left gets a higher priority.
-                if (FS_PRIO_AB && total_rows > 36) {  // long tiles only (C2-size tiles run faster without)
-                    const int left4 = 4 * (total_rows - done0 - r0);  // vs quarters of total_rows
-                    if (left4 > 3 * total_rows) __builtin_amdgcn_s_setprio(3);
-                    else if (left4 > 2 * total_rows) __builtin_amdgcn_s_setprio(2);
-                    else if (left4 > total_rows) __builtin_amdgcn_s_setprio(1);
-                    else __builtin_amdgcn_s_setprio(0);
-                }
-            };
             // general block: rows below H take the masked path (scalar branch per row); refills
             // of rows below H are clamped
             auto block = [&](int r0, auto refill_tag) {
                 constexpr bool kRefill = decltype(refill_tag)::value;
-                prio(r0);
 #pragma unroll
                 for (int i = 0; i < kPrefetch; ++i) {
                     const int r = r0 + i;
@@ -1930,7 +1480,6 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             // need no clamp: one pointer per block, immediate row offsets
             auto lean_block = [&](int r0, auto refill_tag) {
                 constexpr bool kRefill = decltype(refill_tag)::value;
-                prio(r0);
                 const uint32_t* pb = U.gfb + (U.rel0 + kRowDwords * (r0 + kPrefetch));
 #pragma unroll
                 for (int i = 0; i < kPrefetch; ++i) {
@@ -2052,507 +1601,8 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 // geometry (ordering, rows per pass) and header DMA are set up at the current super-tile's
 // last block.
 
-#ifndef FS_PREFETCH_W
-#define FS_PREFETCH_W 6
-#endif
-#ifndef FS_DIAG_W
-#define FS_DIAG_W 0  // diagnostic builds only (wrong results): 1 no combine, 2 no parse, 4 no finish, 8 masked rows lean
-#endif
-#ifdef FS_DIAG_W_DUMP
-__device__ uint32_t g_wdump[kTablesWLdsBytes / 4];
-#endif
-constexpr int kPfW = FS_PREFETCH_W;
-constexpr int kRowDwW = 64;  // 256-byte rows
-
-__device__ __forceinline__ uint32_t zshift_w(const char* lds, uint32_t v, uint32_t k) {
-    for (; k >= 1024u; k -= 1024u) v = zplain(lds, v, kW_Z1024);
-    for (; k >= 256u; k -= 256u) v = zplain(lds, zplain(lds, v, kW_Z192), kW_Z64);
-    if (k >= 192u) { v = zplain(lds, v, kW_Z192); k -= 192u; }
-    else if (k >= 128u) { v = zplain(lds, v, kW_Z128); k -= 128u; }
-    else if (k >= 64u) { v = zplain(lds, v, kW_Z64); k -= 64u; }
-    if (k >= 48u) { v = zplain(lds, v, kW_Z48); k -= 48u; }
-    else if (k >= 32u) { v = zplain(lds, v, kW_Z32); k -= 32u; }
-    else if (k >= 16u) { v = zplain(lds, v, kW_Z16); k -= 16u; }
-    for (; k >= 4u; k -= 4u) v = zplain(lds, v, kW_Zfin);
-    if (k > 0u) v = zplain(lds, v, kW_Zfin + 4096u * (4u - k));
-    return v;
-}
-
-struct LayoutW {
-    static constexpr uint32_t kZfin = kW_Zfin;
-    __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift_w(lds, v, k); }
-    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
-        return zplain(lds, v, kZfin + 4096u * t);
-    }
-    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) { return lds32(lds, kZfin + 3u * 4096u + (i << 2)); }
-};
-
-// Region A in place: entry row e (256 B) = [op*32 + table*8 + copy], op 0 = Z_244, op 1 = Z_4.
-// Thread t writes the 16-B chunk c = t & 15 (op c >> 3, table (c >> 1) & 3) of the rows t >> 4,
-// 64 + (t >> 4), 128 + (t >> 4) and 192 + (t >> 4): the 8 lanes of a ds_write_b128 lane group
-// fill 128 contiguous bytes, so the stores are bank-conflict-free. Each lane loads its table's
-// 8 basis columns (32 B, an L2 hit) with two dwordx4 loads issued before the descriptor and
-// table DMAs; `younger` = the VMEM instructions issued after them (waited for by the caller).
-__device__ __forceinline__ void basis_load_w(const FsTablesW* __restrict__ tabs, u32x4& b0, u32x4& b1) {
-    const uint32_t c = threadIdx.x & 15u;
-    const uint32_t* src = &tabs->basis[c >> 3][(c >> 1) & 3u][0];
-    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:16"
-                 : "=v"(b0), "=v"(b1)
-                 : "v"(src));
-}
-template <int kYounger>
-__device__ __forceinline__ void build_region_w(char* lds, u32x4 b0, u32x4 b1) {
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(b0), "+v"(b1) : "n"(kYounger));
-    const uint32_t t = threadIdx.x;
-    const uint32_t c = t & 15u, e = t >> 4;
-    const uint32_t col[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    uint32_t v = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 6; ++j) v ^= col[j] & (0u - ((e >> j) & 1u));
-    char* base = lds + kW_RegionA + e * 256u + 16u * c;
-    *reinterpret_cast<u32x4*>(base) = u32x4{v, v, v, v};
-    const uint32_t v1 = v ^ col[6], v2 = v ^ col[7], v3 = v1 ^ col[7];
-    *reinterpret_cast<u32x4*>(base + 64u * 256u) = u32x4{v1, v1, v1, v1};
-    *reinterpret_cast<u32x4*>(base + 128u * 256u) = u32x4{v2, v2, v2, v2};
-    *reinterpret_cast<u32x4*>(base + 192u * 256u) = u32x4{v3, v3, v3, v3};
-}
-
-// Z(a) ^ w from region A for the operator whose slot bytes `cvec` holds (Z_244 or Z_4).
-__device__ __forceinline__ uint32_t zrep_w(const char* lds, uint32_t a, uint32_t cvec, const uint32_t (&sel)[4],
-                                           uint32_t w) {
-    const uint32_t t0 = lds32(lds, kW_RegionA + __builtin_amdgcn_perm(a, cvec, sel[0]));
-    const uint32_t t1 = lds32(lds, kW_RegionA + __builtin_amdgcn_perm(a, cvec, sel[1]));
-    const uint32_t t2 = lds32(lds, kW_RegionA + __builtin_amdgcn_perm(a, cvec, sel[2]));
-    const uint32_t t3 = lds32(lds, kW_RegionA + __builtin_amdgcn_perm(a, cvec, sel[3]));
-    return xor3(xor3(t0, t1, t2), t3, w);
-}
-
-struct KeysW {
-    uint32_t c244, c4;  // slot bytes of the lane's copy of each byte table, Z_244 / Z_4
-    uint32_t sel[4];    // v_perm selectors of the 4 lookups (table rotation by lane)
-};
-
-// One row of the lane: A <- Z4(Z4(Z4(Z244(A) ^ w0) ^ w1) ^ w2) ^ w3, and the 4 dwords' sums.
-__device__ __forceinline__ void lean_row_w(const char* lds, const KeysW& k, u32x4 v, uint32_t& A, uint32_t& cs) {
-    A = zrep_w(lds, A, k.c244, k.sel, v.x);
-    A = zrep_w(lds, A, k.c4, k.sel, v.y);
-    A = zrep_w(lds, A, k.c4, k.sel, v.z);
-    A = zrep_w(lds, A, k.c4, k.sel, v.w);
-    cs = sad16(v.x, cs);
-    cs = sad16(v.y, cs);
-    cs = sad16(v.z, cs);
-    cs = sad16(v.w, cs);
-}
-
-// A masked row (masked_row's masks and realignment, one accumulator).
-__device__ __forceinline__ void masked_row_w(const char* lds, const KeysW& k, u32x4 u, int rel, int p, int nd,
-                                             uint32_t sa, uint32_t tail_mask, uint32_t& A, uint32_t& cs) {
-    const uint32_t head_mask = 0xffffffffu << (8u * sa);
-    const int sh = p - rel;
-    uint32_t v[4];
-    v[0] = u.x;
-    v[1] = (sh == 0) ? u.y : u.x;
-    v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
-    v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int x = rel + j;
-        uint32_t d = (x >= 0) ? v[j] : 0u;
-        uint32_t c = 0u;
-        if (x == 0) { d &= head_mask; c = head_mask; }
-        if (x == 1) c = ~head_mask;
-        if (x == nd - 1) d &= tail_mask;
-        A = zrep_w(lds, A, j == 0 ? k.c244 : k.c4, k.sel, d ^ c);
-        cs = sad16(d, cs);
-    }
-}
-
-// The plain tables (44 KB): 3 1-KB LDS-DMA pieces per wave.
-__device__ __forceinline__ void plain_dma_w(const FsTablesW* __restrict__ tabs, const char* lds, uint32_t wave,
-                                            uint32_t lane) {
-    constexpr uint32_t kPieces = kTablesWPlainBytes / 1024u;
-    constexpr uint32_t kPer = (kPieces + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t lds0 = lds_base(lds);
-    const uint32_t w0 = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-        const uint32_t c = min(w0 + k * kWavesPerBlock, kPieces - 1u);
-        dma_x4(reinterpret_cast<const char*>(tabs) + c * 1024u + lane * 16u,
-               __builtin_amdgcn_readfirstlane(lds0 + c * 1024u));
-    }
-}
-
-// Header slots of a super-tile (4-lane mapping: lane (grp, gl) describes frame grp, S / len
-// its descriptor, len 0 for an empty group): frame dwords [0, 16) in the [x >> 2][frame][x & 3]
-// layout. One dwordx4 DMA when every frame spans the slot, else 4 dword DMAs clamped to each
-// frame's last dword. Returns the DMA instruction count (wave-uniform).
-__device__ __forceinline__ int header_dma_w(uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
-                                            const char* lds, uint32_t hw, uint32_t gl, uint32_t lane) {
-    const uint32_t hdr0 = __builtin_amdgcn_readfirstlane(lds_base(lds) + hw);
-    const uint32_t sa = (uint32_t)S & 3u;
-    const int last = (int)((sa + len + 3u) >> 2) - 1;
-    const bool own = len > 0u;
-    const uint64_t fa = reinterpret_cast<uint64_t>(frames + ((S >> 2) << 2));
-    if (__ballot(own && last < kHdrDwW - 1) == 0) {
-        const int src = (int)((lane & 15u) << 4);  // frame (lane & 15)'s lane 0
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)fa);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(fa >> 32));
-        const uint32_t lg = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
-        const uint32_t* fb = reinterpret_cast<const uint32_t*>(((uint64_t)hi << 32) | lo);
-        if (lg > 0u) dma_x4(fb + 4u * (lane >> 4), hdr0);
-        return 1;
-    }
-    if (own) {
-        const uint32_t* fbs = reinterpret_cast<const uint32_t*>(fa);
-#pragma unroll
-        for (int i = 0; i < kHdrDwW / 4; ++i) dma_x1(fbs + min(4 * i + (int)gl, last), hdr0 + 256u * i);
-    }
-    return kHdrDwW / 4;
-}
-
-// The descriptors of super-tile st into the wave's descriptor area by ONE dword LDS-DMA: lanes
-// 0..31 the 16 offsets (two dwords each), lanes 32..47 the 16 lengths (lanes 48..63 re-read the
-// last length); frames past the batch end read the last frame's descriptor.
-__device__ __forceinline__ void desc_dma_w(uint32_t st, uint32_t n, uint32_t fpt, const uint64_t* __restrict__ offsets,
-                                           const uint32_t* __restrict__ lengths, const char* lds, uint32_t dsc,
-                                           uint32_t lane) {
-    const uint32_t f0 = st * fpt;
-    const uint32_t k = lane < 32u ? lane >> 1 : lane < 48u ? lane - 32u : 15u;
-    const uint32_t fi = min(f0 + min(k, fpt - 1u), n - 1u);
-    const void* src = lane < 32u ? static_cast<const void*>(reinterpret_cast<const uint32_t*>(offsets + fi) + (lane & 1u))
-                                 : static_cast<const void*>(lengths + fi);
-    dma_x1(src, __builtin_amdgcn_readfirstlane(lds_base(lds) + dsc));
-}
-
-// Geometry of a super-tile (4-lane mapping; every lane takes part): the frame table, the
-// frames' order by row count (stable), rows and masked head rows per pass, into geometry
-// buffer gb. S / len: this lane's frame (len already without a trailing FCS).
-__device__ __forceinline__ void setup_st(char* lds, uint32_t gb, uint32_t st, uint32_t grp, uint32_t gl, uint32_t n,
-                                         uint32_t fpt, uint64_t S, uint32_t len) {
-    const bool valid = grp < fpt && st * fpt + grp < n;
-    const uint32_t L = valid ? len : 0u;
-    const uint32_t sa = (uint32_t)S & 3u;
-    const int nd = L >= 4u ? (int)((sa + L + 3u) >> 2) : 0;
-    const int rows = (nd + kRowDwW - 1) / kRowDwW;
-    if (gl == 0u) *reinterpret_cast<u32x4*>(lds + gb + 16u * grp) = u32x4{(uint32_t)S, (uint32_t)(S >> 32), L, (uint32_t)nd};
-    // rank of this frame by (rows, index) among the super-tile's fpt slots (rows read by
-    // readlane); slots past fpt keep their index (they are in no pass)
-    int rank = 0;
-#pragma unroll
-    for (int g = 0; g < kFramesPerTile; ++g) {
-        const int rg = __builtin_amdgcn_readlane(rows, 4 * g);
-        rank += (g < (int)fpt && (rg < rows || (rg == rows && g < (int)grp))) ? 1 : 0;
-    }
-    if (grp >= fpt) rank = (int)grp;
-    if (gl == 0u) *reinterpret_cast<uint8_t*>(lds + gb + kW_GeoOrder + rank) = (uint8_t)grp;
-    const int pass = rank >> 2;
-    const int npass = (int)(fpt >> 2);
-    int Pmine = 0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int Pp = group_max(pass == p ? rows : 0);
-        const int Pr = (Pp + kPfW - 1) / kPfW * kPfW;
-        if (pass == p) Pmine = Pr;
-        if ((threadIdx.x & 63u) == 0u) *reinterpret_cast<uint32_t*>(lds + gb + kW_GeoP + 4u * p) = (uint32_t)Pr;
-    }
-    const int need = 2 - (nd - kRowDwW * Pmine);
-    const int h = (nd > 0 && need > 0) ? (need + kRowDwW - 1) / kRowDwW : 0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int Hp = group_max(pass == p ? h : 0);
-        if ((threadIdx.x & 63u) == 0u) *reinterpret_cast<uint32_t*>(lds + gb + kW_GeoH + 4u * p) = (uint32_t)Hp;
-    }
-    if ((threadIdx.x & 63u) == 0u) *reinterpret_cast<uint32_t*>(lds + gb + kW_GeoNpass) = (uint32_t)npass;
-}
-
-// The rows of one pass for this lane (16-lane mapping: group g16 = lane >> 4, lane j in it).
-struct UnitW {
-    const uint32_t* gfb;  // frame dword 0 of the lane's rows (the pass's longest frame for an empty group)
-    int rel0;             // frame dword of this lane's chunk in row 0
-    int lo;               // lowest frame dword a clamped load may start at
-    int P, H;             // wave-uniform: rows (a multiple of kPfW) and leading masked rows
-    int nd;               // the group's own frame: stream dwords (0 = empty or under 4 bytes)
-    uint32_t sa;          // its start alignment
-    uint32_t tail_mask;   // bytes of its last dword inside the frame
-};
-
-__device__ __forceinline__ UnitW unit_w(const char* lds, uint32_t gb, int p, uint32_t g16, uint32_t j,
-                                        const uint8_t* __restrict__ frames) {
-    UnitW U;
-    U.P = (int)__builtin_amdgcn_readfirstlane(lds32(lds, gb + kW_GeoP + 4u * (uint32_t)p));
-    U.H = (int)__builtin_amdgcn_readfirstlane(lds32(lds, gb + kW_GeoH + 4u * (uint32_t)p));
-    const uint32_t f = *reinterpret_cast<const uint8_t*>(lds + gb + kW_GeoOrder + 4u * (uint32_t)p + g16);
-    const uint32_t fm = *reinterpret_cast<const uint8_t*>(lds + gb + kW_GeoOrder + 4u * (uint32_t)p + 3u);
-    const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * f);
-    const u32x4 dm = *reinterpret_cast<const u32x4*>(lds + gb + 16u * fm);
-    U.nd = (int)d.w;
-    const uint64_t S = ((uint64_t)d.y << 32) | d.x;
-    U.sa = (uint32_t)S & 3u;
-    const uint32_t e = (U.sa + d.z) & 3u;
-    U.tail_mask = e ? ((1u << (8u * e)) - 1u) : 0xffffffffu;
-    const bool own = U.nd > 0;
-    const uint64_t ls = own ? S : (((uint64_t)dm.y << 32) | dm.x);
-    const int lnd = own ? U.nd : (int)dm.w;
-    const uint64_t sdw = ls >> 2;
-    U.gfb = reinterpret_cast<const uint32_t*>(frames + (sdw << 2));
-    U.rel0 = lnd - kRowDwW * U.P + 4 * (int)j;
-    U.lo = max(sdw > (1u << 24) ? -(1 << 24) : -(int)sdw, min(0, lnd - 4));
-    return U;
-}
-
-__device__ __forceinline__ void prefetch_w(const UnitW& U, u32x4 (&pf)[kPfW]) {
-#pragma unroll
-    for (int i = 0; i < kPfW; ++i) {
-        const int rel = U.rel0 + kRowDwW * i;
-        pf[i] = load_row(U.gfb, i < U.H ? load_pos(rel, U.lo) : rel);
-    }
-}
-
-// The 16-lane combine of a pass: A ^ junk per lane, Z_(16(3 - (j & 3))) per lane and a quad
-// XOR, Z_(64(3 - (j >> 2))) per quad and an XOR over the quads (DPP row_ror 4 and 8); the
-// checksum partials folded and summed likewise.
-__device__ __forceinline__ void combine_w(const char* lds, uint32_t j, uint32_t A, uint32_t cs, uint32_t junk,
-                                          uint32_t& Y, uint32_t& csum) {
-    const uint32_t U = A ^ junk;
-    cs -= sad16(junk, 0u);
-    const uint32_t w = j & 3u, q = j >> 2;
-    uint32_t y = zplain(lds, U, w == 0u ? kW_Z48 : w == 1u ? kW_Z32 : kW_Z16);
-    if (w == 3u) y = U;
-    y ^= dpp_quad<kQuadXor1>(y);
-    y ^= dpp_quad<kQuadXor2>(y);
-    uint32_t z = zplain(lds, y, q == 0u ? kW_Z192 : q == 1u ? kW_Z128 : kW_Z64);
-    if (q == 3u) z = y;
-    z ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)z, 0x124, 0xf, 0xf, false);  // row_ror:4
-    z ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)z, 0x128, 0xf, 0xf, false);  // row_ror:8
-    cs = (cs & 0xffffu) + (cs >> 16);
-    cs += dpp_quad<kQuadXor1>(cs);
-    cs += dpp_quad<kQuadXor2>(cs);
-    cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0x124, 0xf, 0xf, false);
-    cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0x128, 0xf, 0xf, false);
-    Y = z;
-    csum = cs;
-}
-
-// vmcnt(N) tied to registers loaded by inline asm (no use is scheduled above it).
-template <int N>
-__device__ __forceinline__ void wait_tied(uint64_t& S, uint32_t& len) {
-    if (N == 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(S), "+v"(len));
-    else asm volatile("s_waitcnt vmcnt(%2)" : "+v"(S), "+v"(len) : "n"(N));
-}
-
-template <uint32_t kOps>
-__global__ void __launch_bounds__(kThreads, 1)
-digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
-                const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTablesW* __restrict__ tabs,
-                uint2* __restrict__ out, uint8_t* __restrict__ status, uint8_t* wframes, uint32_t tx, uint32_t fpt) {
-    char* lds = g_lds;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-    fpt = __builtin_amdgcn_readfirstlane(fpt);
-    const uint32_t nst = (n + fpt - 1) / fpt;
-    const uint32_t hw = kW_Hdr + wave * kHdrWaveW;
-    const uint32_t wb = kW_Wave + wave * kW_WaveBytes;
-    const uint32_t pk = wb + kW_Park;
-
-    KeysW keys;
-    {
-        const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
-        keys.c244 = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) keys.c244 |= (32u * j + 4u * c) << (8u * j);
-        keys.c4 = keys.c244 + 0x80808080u;  // op 1 = slots 32..63 (+128 bytes)
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t b = (k + h) & 3u;
-            keys.sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
-        }
-    }
-
-    uint32_t st = wave * gridDim.x + blockIdx.x;  // wave-major first super-tile
-    u32x4 pf[kPfW];
-    const uint32_t dsc = wb + kW_Desc;  // the next super-tile's descriptors, DMA'd one super-tile ahead
-    uint32_t gb = wb + kW_Geo;  // geometry buffer of the super-tile being consumed
-    bool pre = false;           // the current pass's first rows are in the ring
-    {
-        const uint32_t grp = lane >> 2, gl = lane & 3u;
-        uint64_t S = 0;
-        uint32_t len = 0;
-        const bool first = st < nst;
-        u32x4 b0, b1;
-        basis_load_w(tabs, b0, b1);
-        if (first) tile_descriptors(st, grp, n, offsets, lengths, S, len, fpt);
-        plain_dma_w(tabs, lds, wave, lane);
-#ifdef FS_DIAG_W_DMA_A
-        {  // diagnostic: region A copied from the host-built image instead of built in place
-            const uint32_t lds0 = lds_base(lds);
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t c = wave + 16u * k;
-                dma_x4(reinterpret_cast<const char*>(tabs) + kTablesWPlainBytes + c * 1024u + lane * 16u,
-                       __builtin_amdgcn_readfirstlane(lds0 + kW_RegionA + c * 1024u));
-            }
-        }
-#else
-        build_region_w<3>(lds, b0, b1);  // younger: the 3 table pieces (and the 2 descriptor loads)
-#endif
-        wait_tied<0>(S, len);
-        if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
-        if (first) {
-            setup_st(lds, gb, st, grp, gl, n, fpt, S, len);
-            const bool valid = grp < fpt && st * fpt + grp < n;
-            header_dma_w(S, valid ? len : 0u, frames, lds, hw, gl, lane);
-            if (st + nwaves < nst) desc_dma_w(st + nwaves, n, fpt, offsets, lengths, lds, dsc, lane);
-            const UnitW U0 = unit_w(lds, gb, 0, lane >> 4, lane & 15u, frames);
-            if (U0.P > 0) {
-                prefetch_w(U0, pf);
-                pre = true;
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): region A and the geometry are in LDS
-        __builtin_amdgcn_s_barrier();        // tables ready (no vmcnt drain)
-#ifdef FS_DIAG_W_DUMP
-        if (blockIdx.x == 0) {  // diagnostic: workgroup 0's table image
-            for (uint32_t i = threadIdx.x; i < kTablesWLdsBytes / 4; i += kThreads)
-                g_wdump[i] = lds32(lds, 4u * i);
-        }
-#endif
-        if (FS_AGE_PRIO) {
-            const uint32_t w = wave >> 2;
-            if (w == 3u) __builtin_amdgcn_s_setprio(3);
-            else if (w == 2u) __builtin_amdgcn_s_setprio(2);
-            else if (w == 1u) __builtin_amdgcn_s_setprio(1);
-        }
-    }
-
-    while (st < nst) {
-        const int npass = (int)__builtin_amdgcn_readfirstlane(lds32(lds, gb + kW_GeoNpass));
-        const uint32_t gnext = gb == wb + kW_Geo ? wb + kW_Geo + kW_GeoBytes : wb + kW_Geo;  // the other buffer
-        // ---- header parse of the whole super-tile (4-lane mapping), inlined, before its rows: the
-        // header DMA was issued before the ring's kPfW loads of its first rows (or before everything)
-        {
-            if (pre) __builtin_amdgcn_s_waitcnt(0x0070 | kPfW);
-            else __builtin_amdgcn_s_waitcnt(0x0070);
-            const uint32_t grp = lane >> 2, gl = lane & 3u;
-            const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * grp);
-            const uint64_t S = ((uint64_t)d.y << 32) | d.x;
-            const bool valid = grp < fpt && st * fpt + grp < n;
-            if (!(FS_DIAG_W & 2))
-                parse_tile_body<kOps, kHdrDwW>(hw, grp, gl, (uint32_t)S & 3u, d.z, mtu,
-                                               reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
-                                               valid && gl == 0u, pk);
-        }
-        bool next_ready = false;
-        // the next super-tile: geometry, header DMA (the slot is free: parsed above), the
-        // descriptors of the one after, its first unit
-        auto setup_next = [&](bool in_block) -> UnitW {
-            // the descriptor DMA is older than the ring's kPfW youngest loads (or than everything)
-            if (in_block) __builtin_amdgcn_s_waitcnt(0x0070 | kPfW);
-            else __builtin_amdgcn_s_waitcnt(0x0070);
-            const uint32_t grp = lane >> 2, gl = lane & 3u;
-            const uint64_t S = *reinterpret_cast<const uint64_t*>(lds + dsc + 8u * grp);
-            uint32_t len = *reinterpret_cast<const uint32_t*>(lds + dsc + kW_DescLen + 4u * grp);
-            if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
-            const uint32_t stn = st + nwaves;
-            setup_st(lds, gnext, stn, grp, gl, n, fpt, S, len);
-            const bool valid = grp < fpt && stn * fpt + grp < n;
-            header_dma_w(S, valid ? len : 0u, frames, lds, hw, gl, lane);
-            if (stn + nwaves < nst) desc_dma_w(stn + nwaves, n, fpt, offsets, lengths, lds, dsc, lane);
-            next_ready = true;
-            return unit_w(lds, gnext, 0, lane >> 4, lane & 15u, frames);
-        };
-
-        for (int p = 0; p < npass; ++p) {
-            const uint32_t j = lane & 15u;
-            const UnitW U = unit_w(lds, gb, p, lane >> 4, j, frames);
-            uint32_t A = 0u, cs = 0u;
-            if (U.P > 0 && !pre) prefetch_w(U, pf);
-            pre = false;
-            // the pass's last dword (lane 15's 4th of the last row) holds up to 3 bytes past
-            // the frame end: masked in the last block (a masked last row masks it itself)
-            const uint32_t endmask = (j == 15u && U.nd > 0 && U.H < U.P) ? U.tail_mask : 0xffffffffu;
-            for (int r0 = 0; r0 < U.P; r0 += kPfW) {
-                const bool lastb = r0 + kPfW == U.P;
-                // the refills: this unit's rows kPfW ahead, or (last block) the next unit's first
-                // rows -- the next pass's, the next super-tile's, or (none left) this unit's own
-                // first rows again (harmless cache hits): ONE load per ring slot on every path, so
-                // the compiler never copies an in-flight register
-                const uint32_t* rb = U.gfb;  // refill rows: frame base, first row's dword, clamp floor,
-                int rrel = U.rel0 + kRowDwW * (r0 + kPfW), rlo = U.lo, rH = U.H - (r0 + kPfW);  // clamped rows
-                if (lastb) {
-                    UnitW Nx;
-                    Nx.P = 0;
-                    if (p + 1 < npass) Nx = unit_w(lds, gb, p + 1, lane >> 4, j, frames);
-                    else if (st + nwaves < nst) Nx = setup_next(true);
-                    pre = Nx.P > 0;
-                    if (!pre) Nx = U;
-                    rb = Nx.gfb;
-                    rrel = Nx.rel0;
-                    rlo = Nx.lo;
-                    rH = Nx.H;
-                }
-                const uint32_t* pb = rb + rrel;
-#pragma unroll
-                for (int i = 0; i < kPfW; ++i) {
-                    const int r = r0 + i;
-                    const int rel = U.rel0 + kRowDwW * r;
-                    if (r < U.H && !(FS_DIAG_W & 8)) {
-                        masked_row_w(lds, keys, pf[i], rel, load_pos(rel, U.lo), U.nd, U.sa, U.tail_mask, A, cs);
-                    } else if (i == kPfW - 1) {
-                        u32x4 v = pf[i];
-                        v.w &= lastb ? endmask : 0xffffffffu;
-                        lean_row_w(lds, keys, v, A, cs);
-                    } else {
-                        lean_row_w(lds, keys, pf[i], A, cs);
-                    }
-                    if (i < rH) pf[i] = load_row(rb, load_pos(rrel + kRowDwW * i, rlo));  // wave-uniform branch
-                    else pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwW * i);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            // combine the pass
-            if (U.P == 0) A = cs = 0u;
-            uint32_t Y = A, csum = cs;
-            if (!(FS_DIAG_W & 1)) combine_w(lds, j, A, cs, 0u, Y, csum);
-            if (j == 0u) {
-                const uint32_t f = *reinterpret_cast<const uint8_t*>(lds + gb + kW_GeoOrder + 4u * (uint32_t)p + (lane >> 4));
-                *reinterpret_cast<uint2*>(lds + wb + kW_Ycs + 8u * f) = make_uint2(Y, csum);
-            }
-        }
-        if (!next_ready && st + nwaves < nst) {
-            const UnitW Un = setup_next(false);
-            if (Un.P > 0) {
-                prefetch_w(Un, pf);
-                pre = true;
-            }
-        }
-        // ---- finish the super-tile (4-lane mapping: the group's lane 0 finishes its frame)
-        {
-            uint32_t ln;
-            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-            const uint32_t grp = ln >> 2, gl = ln & 3u;
-            const bool valid = grp < fpt && st * fpt + grp < n;
-            if (valid && gl == 0u && !(FS_DIAG_W & 4)) {
-                const u32x4 d = *reinterpret_cast<const u32x4*>(lds + gb + 16u * grp);
-                const uint64_t S = ((uint64_t)d.y << 32) | d.x;
-                const uint32_t len = d.z;
-                const uint32_t e = (((uint32_t)S & 3u) + len) & 3u;
-                const uint2 yc = *reinterpret_cast<const uint2*>(lds + wb + kW_Ycs + 8u * grp);
-                finish_frame<kOps, LayoutW>(lds, unpark_parsed<kOps>(lds, pk, grp), S, len, e ? e : 4u, yc.x, yc.y,
-                                            frames, wframes, lengths, st * fpt + grp, out, status, tx);
-            }
-        }
-        st += nwaves;
-        gb = gnext;
-    }
-}
-
 }  // namespace
 
-#ifdef FS_DIAG_W_DUMP
-extern "C" int fs_debug_read_wdump(void* host, size_t bytes) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wdump), bytes, 0, hipMemcpyDeviceToHost);
-}
-#endif
 #ifdef FS_STAMPS
 extern "C" int fs_debug_read_stamps(void* host, size_t bytes) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fs_stamps), bytes, 0, hipMemcpyDeviceToHost);
@@ -2561,8 +1611,8 @@ extern "C" int fs_debug_read_stamps(void* host, size_t bytes) {
 
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
-                         int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, int force, FsOp op,
-                         uint8_t* wframes, uint32_t tx, const FsTablesW* tables_w) {
+                         int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, uint32_t* next_id,
+                         int force, FsOp op, uint8_t* wframes, uint32_t tx) {
     if (n == 0) return hipSuccess;
     const uint32_t max_blocks = (uint32_t)(num_cus > 0 ? num_cus : 256);
     // The report of the launches before (the latest launch id that met a mixed-length tile):
@@ -2571,9 +1621,10 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     // reporting while the traffic is mixed). A heuristic only: never a result.
     // Launch ids are 16-bit (they travel in the report pointer's top bits; 0 = never reported).
     constexpr uint32_t kStickyLaunches = 4096;
-    static std::atomic<uint32_t> next_id{1};
-    uint32_t id = next_id.fetch_add(1) & 0xFFFFu;
-    if (id == 0u) id = next_id.fetch_add(1) & 0xFFFFu;
+    // (the counter is the context's: another context's launches never shift this one's window;
+    // a context is used from one thread at a time, include/framesum.h)
+    uint32_t id = (*next_id)++ & 0xFFFFu;
+    if (id == 0u) id = (*next_id)++ & 0xFFFFu;
     const uint64_t rdev = reinterpret_cast<uint64_t>(report_dev);
     const bool can_report = report_host && rdev != 0u && (rdev >> 48) == 0u;
     const uint64_t report = can_report ? rdev | ((uint64_t)id << 48) : 0u;
@@ -2591,7 +1642,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
             mixed = true;
         }
     }
-    if (force) mixed = force == 2;
+    if (force) mixed = force == 2;  // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {
         if (report_host) report_host[kReportChosen] = v;
@@ -2606,53 +1657,22 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     uint32_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     uint2* o = reinterpret_cast<uint2*>(out);
-    if (force == 3 && tables_w) {
-#define FS_LAUNCH_W(OPS)                                                                                       \
-    hipLaunchKernelGGL((digest_kernel_w<OPS>), dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, \
-                       mtu, tables_w, o, status, wframes, tx, fpt)
-        chosen(3u);
-        switch (op) {
-        case FsOp::kDigest: FS_LAUNCH_W(kOpsDigest); break;
-        case FsOp::kFill: FS_LAUNCH_W(kOpsTx); break;
-        case FsOp::kFcs: FS_LAUNCH_W(kOpsFcs); break;
-        }
-#undef FS_LAUNCH_W
-        return hipGetLastError();
-    }
 #define FS_LAUNCH(K)                                                                                        \
     hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
-    const bool al = force == 0 || force == 4 || force == 5;  // the one-pass choice: block-aligned rows (force 1: end-anchored)
-    // force 5: the block-aligned kernel as two 8-wave workgroups per CU (LayA2; RX ops only)
-    const bool dual = force == 5 && op != FsOp::kFill;
-    if (dual && !mixed) {
-        uint32_t b2 = (tiles + kA2Waves - 1) / kA2Waves;
-        if (b2 > 2u * max_blocks) b2 = 2u * max_blocks;
-#define FS_LAUNCH2(OPS)                                                                                         \
-    hipLaunchKernelGGL((digest_kernel_a<OPS, true, LayA2>), dim3(b2), dim3(kA2Waves * kWave), 0, stream, frames, offsets, \
-                       lengths, n, mtu, tables, o, status, report, wframes, tx, fpt)
-        chosen(5u);
-        if (op == FsOp::kDigest) FS_LAUNCH2(kOpsDigest);
-        else FS_LAUNCH2(kOpsFcs);
-#undef FS_LAUNCH2
-        return hipGetLastError();
-    }
-    chosen(mixed ? 2u : al ? 4u : 1u);
+    chosen(mixed ? 2u : 4u);
     switch (op) {
     case FsOp::kDigest:
         if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
-        else if (al) FS_LAUNCH((digest_kernel_a<kOpsDigest, true>));
-        else FS_LAUNCH((digest_kernel_a<kOpsDigest, false>));
+        else FS_LAUNCH((digest_kernel_a<kOpsDigest>));
         break;
     case FsOp::kFill:
         if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
-        else if (al) FS_LAUNCH((digest_kernel_a<kOpsTx, true>));
-        else FS_LAUNCH((digest_kernel_a<kOpsTx, false>));
+        else FS_LAUNCH((digest_kernel_a<kOpsTx>));
         break;
     case FsOp::kFcs:
         if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
-        else if (al) FS_LAUNCH((digest_kernel_a<kOpsFcs, true>));
-        else FS_LAUNCH((digest_kernel_a<kOpsFcs, false>));
+        else FS_LAUNCH((digest_kernel_a<kOpsFcs>));
         break;
     }
 #undef FS_LAUNCH

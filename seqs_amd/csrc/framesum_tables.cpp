@@ -43,14 +43,6 @@ void build_tables(FsTables* t) {
     for (uint32_t e = 0; e < 256; ++e)
         for (uint32_t b = 0; b < 4; ++b)
             for (uint32_t c = 0; c < 8; ++c) t->region_a[e][8 * b + c] = zrow[b][e];
-    for (int k = 0; k < 8; ++k) {  // the two-workgroups-per-CU kernel's plain tables
-        static uint32_t zk[4][256];
-        op_table(t1, kA2Tables[k], zk);
-        for (uint32_t e = 0; e < 256; ++e)
-            for (uint32_t b = 0; b < 4; ++b) t->region_a[e][32u + ((4u * k + b) ^ (e & 31u))] = zk[b][e];
-        for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t j = 0; j < 8; ++j) t->a2_basis[4 * k + b][j] = zk[b][1u << j];
-    }
     for (uint32_t b = 0; b < 4; ++b)
         for (uint32_t j = 0; j < 8; ++j) t->z64_basis[b][j] = zrow[b][1u << j];
     // region A entries are the XOR of the basis columns of their set bits (GF(2) linearity)
@@ -81,71 +73,6 @@ void build_tables(FsTables* t) {
         }
     // The final step Z_(4-t) replaces "Z_4 then undo t appended zero bytes"; Z_1[0] is the
     // standard byte table used for frames shorter than 4 bytes.
-    if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");
-}
-
-void build_tables_rx(FsTablesRx* t) {
-    std::memset(t, 0, sizeof(*t));
-    uint32_t t1[256];
-    byte_table(t1);
-    static uint32_t z[4][256];
-    op_table(t1, 256, z);
-    for (uint32_t b = 0; b < 4; ++b)
-        for (uint32_t j = 0; j < 8; ++j) t->z256_basis[b][j] = z[b][1u << j];
-    for (uint32_t k = 0; k < 8; ++k) {
-        op_table(t1, kRxPlain[k], z);
-        for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t j = 0; j < 8; ++j) t->plain_basis[4 * k + b][j] = z[b][1u << j];
-    }
-    // the standard byte table is Z_4's byte-3 table (the finish's tail bytes use it)
-    op_table(t1, 4, z);
-    if (std::memcmp(z[3], t1, sizeof(t1)) != 0) throw std::logic_error("Z_4 byte-3 table is not the CRC table");
-}
-
-void rx_region_image(const FsTablesRx* t, uint32_t region[256][64]) {
-    auto lin = [](const uint32_t basis[8], uint32_t e) {
-        uint32_t v = 0;
-        for (uint32_t j = 0; j < 8; ++j)
-            if ((e >> j) & 1u) v ^= basis[j];
-        return v;
-    };
-    for (uint32_t e = 0; e < 256; ++e) {
-        for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t c = 0; c < 8; ++c) region[e][8 * b + c] = lin(t->z256_basis[b], e);
-        for (uint32_t q = 0; q < 32; ++q) region[e][32u + (q ^ (e >> 3))] = lin(t->plain_basis[q], e);
-    }
-}
-
-void build_tables_w(FsTablesW* t) {
-    std::memset(t, 0, sizeof(*t));
-    uint32_t t1[256];
-    byte_table(t1);
-    static uint32_t zop[2][4][256];
-    op_table(t1, 244, zop[0]);
-    op_table(t1, 4, zop[1]);
-    for (uint32_t o = 0; o < 2; ++o)
-        for (uint32_t e = 0; e < 256; ++e)
-            for (uint32_t b = 0; b < 4; ++b)
-                for (uint32_t c = 0; c < 8; ++c) t->region_a[e][32 * o + 8 * b + c] = zop[o][b][e];
-    for (uint32_t o = 0; o < 2; ++o)
-        for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t j = 0; j < 8; ++j) t->basis[o][b][j] = zop[o][b][1u << j];
-    for (uint32_t o = 0; o < 2; ++o)
-        for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t e = 0; e < 256; ++e) {
-                uint32_t v = 0;
-                for (uint32_t j = 0; j < 8; ++j)
-                    if ((e >> j) & 1u) v ^= t->basis[o][b][j];
-                if (v != zop[o][b][e]) throw std::logic_error("region A basis mismatch");
-            }
-    op_table(t1, 16, t->z16);
-    op_table(t1, 32, t->z32);
-    op_table(t1, 48, t->z48);
-    op_table(t1, 64, t->z64);
-    op_table(t1, 128, t->z128);
-    op_table(t1, 192, t->z192);
-    for (int k = 0; k < 4; ++k) op_table(t1, 4 - k, t->zfin[k]);
-    op_table(t1, 1024, t->z1024);
     if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");
 }
 

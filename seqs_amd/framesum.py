@@ -197,18 +197,17 @@ class Engine:
             raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
 
     # kernel variants (fs_ctx_set_kernel): results are identical, only the speed differs
-    KERNEL_AUTO, KERNEL_ONE_PASS, KERNEL_MIXED, KERNEL_WIDE, KERNEL_ALIGNED, KERNEL_DUAL, KERNEL_STREAM = 0, 1, 2, 3, 4, 5, 6
+    KERNEL_AUTO, KERNEL_MIXED, KERNEL_ONE_PASS = 0, 2, 4
 
     def set_kernel(self, variant: int) -> None:
-        """0: automatic (the mixed-length kernel after a batch that had mixed-length tiles, the
-        block-aligned one-pass kernel otherwise); 1: the one-pass kernel with end-anchored rows;
-        2: the kernel that splits long frames of mixed-length tiles into pieces; 3: the 16-lane
-        kernel (256-byte rows, frames ordered by length into passes); 4: the one-pass kernel with
-        block-aligned rows; 5: the same as two 8-wave workgroups per CU (RX ops)."""
+        """0 (KERNEL_AUTO): automatic (the mixed-length kernel after a batch that had mixed-length
+        tiles, the one-pass kernel otherwise); 2 (KERNEL_MIXED): the kernel that splits long frames
+        of mixed-length tiles into pieces; 4 (KERNEL_ONE_PASS): the one-pass kernel (block-aligned
+        rows). Any other value raises."""
         self._check(self.lib.fs_ctx_set_kernel(self._ctx, int(variant)), "fs_ctx_set_kernel")
 
     def last_kernel(self) -> int:
-        """The variant (1..5) this context's latest launch ran (0 before its first launch). With
+        """The variant (2 or 4) this context's latest launch ran (0 before its first launch). With
         variant 0 the first 16 launches run the mixed-length kernel (2); it stays chosen while its
         batches have mixed-length tiles, uniform traffic then moves to the one-pass kernel (4)."""
         v = self.lib.fs_ctx_last_kernel(self._ctx)

@@ -149,123 +149,8 @@ def fold_native_to_be(total: int, parity: int) -> int:
     return r
 
 
-# ---- the wide-group kernel (digest_kernel_w): 16 lanes per frame, end-anchored 256-byte rows,
-# A <- Z256(A) ^ w per dword stream, the combine U = Z12(A0)^Z8(A1)^Z4(A2)^A3 per lane, then
-# Z_(16(3-(j&3))) per lane and a quad XOR, then Z_(64(3-(j>>2))) per quad and an XOR over the
-# quads, then the final Z_(4-t).
-Z256, Z12, Z8, Z48 = op_table(256), op_table(12), op_table(8), op_table(48)
-Z64Q, Z128, Z192 = Z64, op_table(128), op_table(192)
-
-
-def crc32_model_w(buf: bytes, S: int, length: int) -> int:
-    E = S + length
-    if length < 4:
-        return crc32_model(buf, S, length)
-    sdw = S >> 2
-    nd = ((E + 3) >> 2) - sdw
-    sa = S & 3
-    te = (E & 3) or 4
-    head_mask = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
-    tail_mask = 0xFFFFFFFF if te == 4 else (1 << (8 * te)) - 1
-    padded = bytes(buf) + b"\0" * 8
-
-    def dword(rel):
-        return struct.unpack_from("<I", padded, 4 * (sdw + rel))[0]
-
-    R = (nd + 63) // 64
-    A = [[0] * 4 for _ in range(16)]
-    for r in range(R):
-        for lane in range(16):
-            rel = nd - 64 * R + 64 * r + 4 * lane
-            for j in range(4):
-                rj = rel + j
-                dc = 0
-                if rj >= 0:
-                    mk, x = 0xFFFFFFFF, 0
-                    if rj == 0:
-                        mk &= head_mask
-                        x ^= head_mask
-                    if rj == 1:
-                        x ^= (~head_mask) & 0xFFFFFFFF
-                    if rj == nd - 1:
-                        mk &= tail_mask
-                    dc = (dword(rj) & mk) ^ x
-                A[lane][j] = apply(Z256, A[lane][j]) ^ dc
-    quad_tab = [Z48, Z32, Z16, None]
-    quad_level = [Z192, Z128, Z64Q, None]
-    Y = 0
-    for q in range(4):
-        W = 0
-        for w in range(4):
-            lane = 4 * q + w
-            a = A[lane]
-            u = apply(Z12, a[0]) ^ apply(Z8, a[1]) ^ apply(Z4, a[2]) ^ a[3]
-            W ^= u if quad_tab[w] is None else apply(quad_tab[w], u)
-        Y ^= W if quad_level[q] is None else apply(quad_level[q], W)
-    t = (4 - (E & 3)) & 3
-    return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
-
-
-# ---- the 16-lane kernel with ONE stream per lane: each 256-byte row folds the lane's 4 dwords
-# into its accumulator by A <- Z4(Z4(Z4(Z244(A) ^ w0) ^ w1) ^ w2) ^ w3 (= Z256(A) ^ Z12(w0) ^
-# Z8(w1) ^ Z4(w2) ^ w3), so the combine only folds 16 lane values per frame.
-Z244 = op_table(244)
-
-
-def crc32_model_w1(buf: bytes, S: int, length: int) -> int:
-    E = S + length
-    if length < 4:
-        return crc32_model(buf, S, length)
-    sdw = S >> 2
-    nd = ((E + 3) >> 2) - sdw
-    sa = S & 3
-    te = (E & 3) or 4
-    head_mask = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
-    tail_mask = 0xFFFFFFFF if te == 4 else (1 << (8 * te)) - 1
-    padded = bytes(buf) + b"\0" * 8
-
-    def dword(rel):
-        return struct.unpack_from("<I", padded, 4 * (sdw + rel))[0]
-
-    R = (nd + 63) // 64
-    A = [0] * 16
-    for r in range(R):
-        for lane in range(16):
-            rel = nd - 64 * R + 64 * r + 4 * lane
-            d = []
-            for j in range(4):
-                rj = rel + j
-                dc = 0
-                if rj >= 0:
-                    mk, x = 0xFFFFFFFF, 0
-                    if rj == 0:
-                        mk &= head_mask
-                        x ^= head_mask
-                    if rj == 1:
-                        x ^= (~head_mask) & 0xFFFFFFFF
-                    if rj == nd - 1:
-                        mk &= tail_mask
-                    dc = (dword(rj) & mk) ^ x
-                d.append(dc)
-            a = apply(Z244, A[lane]) ^ d[0]
-            a = apply(Z4, a) ^ d[1]
-            a = apply(Z4, a) ^ d[2]
-            A[lane] = apply(Z4, a) ^ d[3]
-    quad_tab = [Z48, Z32, Z16, None]
-    quad_level = [Z192, Z128, Z64Q, None]
-    Y = 0
-    for q in range(4):
-        W = 0
-        for w in range(4):
-            u = A[4 * q + w]
-            W ^= u if quad_tab[w] is None else apply(quad_tab[w], u)
-        Y ^= W if quad_level[q] is None else apply(quad_level[q], W)
-    t = (4 - (E & 3)) & 3
-    return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
-
-
 def crc32_model_al(buf: bytes, S: int, length: int, base_phase: int = 0) -> int:
-    """digest_kernel_a<kOps, true>: BLOCK-ALIGNED 64-byte rows (the last row ends on the 64-B
+    """digest_kernel_a (the one-pass kernel): BLOCK-ALIGNED 64-byte rows (the last row ends on the 64-B
     block after the frame end; base_phase = absolute dword phase of buf[0] within a block),
     the stream dwords past the frame end leave their stream untouched, and the combine shifts
     stream (lane, j) by 4 * ((q - 4 lane - j) mod 16) bytes, q = the frame's last dword's
@@ -316,94 +201,3 @@ def crc32_model_al(buf: bytes, S: int, length: int, base_phase: int = 0) -> int:
             Y ^= v
     t = (4 - (E & 3)) & 3
     return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
-
-
-# ---- the streaming kernel (seqs_amd/csrc/framesum_rx.hip) ---------------------------------
-Z256, Z1536, Z48, Z128, Z192 = op_table(256), op_table(1536), op_table(48), op_table(128), op_table(192)
-RX_PR, RX_PIECE = 6, 1536
-
-
-def rx_geometry(S: int, slen: int):
-    """(D, R, npc, h) of a frame as the streaming kernel cuts it (npc 0: bytewise)."""
-    E = S + slen
-    Ed, F4 = E & ~3, S & ~3
-    if slen < 4 or Ed < S + 4:
-        return 0, 0, 0, 0
-    D = (Ed - F4) // 4
-    R = (D + 63) // 64
-    npc = (R + RX_PR - 1) // RX_PR
-    return D, R, npc, R - RX_PR * (npc - 1)
-
-
-def crc32_model_rx(buf: bytes, S: int, slen: int, base: int = 0) -> int:
-    """CRC-32 of buf[S:S+slen] computed the way framesum_rx.hip does: end-anchored 1536-B pieces
-    of 256-B rows, 16 lanes x 4 dword streams with A <- Z256(A) ^ w, the head row's clamp to the
-    16-B block holding the first byte (at absolute address base + S) and its realignment, the
-    Z4 Horner per lane, the quad and row trees, the Z1536 fold over pieces, Z4 and the tail bytes."""
-    E = S + slen
-    Ed, F4 = E & ~3, S & ~3
-    D, R, npc, h = rx_geometry(S, slen)
-    if npc == 0:
-        c = 0xFFFFFFFF
-        for b in buf[S:E]:
-            c = T1[(c ^ b) & 0xFF] ^ (c >> 8)
-        return c ^ 0xFFFFFFFF
-    pad = 64
-    mem = bytes(pad) + bytes(buf) + bytes(64)  # mem[pad + a] = buf[a]
-
-    def dw(a):
-        return struct.unpack_from("<I", mem, pad + a)[0]
-
-    lo = ((base + S) & ~15) - base  # buffer-relative clamp address
-    xl = (lo - F4) // 4
-    sa = S & 3
-    hm = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
-    C = 0
-    for p in range(npc):
-        pe = Ed - RX_PIECE * (npc - 1 - p)
-        A = [[0] * 4 for _ in range(16)]
-        u0 = RX_PR - h if p == 0 else 0
-        for u in range(u0, RX_PR):
-            for gl in range(16):
-                a = pe - RX_PIECE + 256 * u + 16 * gl
-                if p == 0:
-                    x = (a - F4) // 4
-                    al = max(a, lo)
-                    sh = min(max(xl - x, 0), 4)
-                    raw = [dw(al + 4 * j) for j in range(4)]
-                    v = [raw[j - sh] if j >= sh else 0 for j in range(4)]
-                    for j in range(4):
-                        xj = x + j
-                        d = v[j] if xj >= 0 else 0
-                        ci = 0
-                        if xj == 0:
-                            d &= hm
-                            ci = hm
-                        if xj == 1:
-                            ci = hm ^ 0xFFFFFFFF
-                        A[gl][j] = apply(Z256, A[gl][j]) ^ d ^ ci
-                else:
-                    for j in range(4):
-                        A[gl][j] = apply(Z256, A[gl][j]) ^ dw(a + 4 * j)
-        U = []
-        for gl in range(16):
-            t = apply(Z4, A[gl][0]) ^ A[gl][1]
-            t = apply(Z4, t) ^ A[gl][2]
-            U.append(apply(Z4, t) ^ A[gl][3])
-        quad = [Z48, Z32, Z16, None]
-        row = [Z192, Z128, Z64, None]
-        W = 0
-        for q in range(4):
-            qs = 0
-            for r in range(4):
-                u = U[4 * q + r]
-                qs ^= u if quad[r] is None else apply(quad[r], u)
-            W ^= qs if row[q] is None else apply(row[q], qs)
-        C = W if p == 0 else apply(Z1536, C) ^ W
-    reg = apply(Z4, C)
-    if npc > 1 and D - 384 * (npc - 1) == 1 and sa:
-        # frame dword 1 opens piece 1: its part of the CRC init, linear, added here
-        reg ^= zero_shift(apply(Z4, hm ^ 0xFFFFFFFF), 4 * D - 8)
-    for b in buf[Ed:E]:
-        reg = (reg >> 8) ^ T1[(reg ^ b) & 0xFF]
-    return reg ^ 0xFFFFFFFF

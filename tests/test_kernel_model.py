@@ -85,45 +85,3 @@ def test_block_aligned_rows_vs_zlib():
         pre = rnd.randrange(0, 70)
         buf = rnd.randbytes(pre + L + 8)
         assert km.crc32_model_al(buf, pre, L, rnd.randrange(16)) == zlib.crc32(buf[pre : pre + L])
-
-
-def test_16_lane_models_vs_zlib():
-    rnd = random.Random(13)
-    for _ in range(150):
-        L = rnd.choice([4, 5, 255, 256, 257, 1500, rnd.randrange(4, 3000)])
-        pre = rnd.randrange(0, 13)
-        buf = rnd.randbytes(pre + L + 8)
-        assert km.crc32_model_w(buf, pre, L) == zlib.crc32(buf[pre : pre + L])
-        assert km.crc32_model_w1(buf, pre, L) == zlib.crc32(buf[pre : pre + L])
-
-
-def test_streaming_kernel_model_vs_zlib():
-    # framesum_rx.hip: end-anchored 1536-B pieces of 256-B rows, head pieces of 1..6 rows, the
-    # clamp of chunks before the frame to the 16-B block of its first byte at every absolute base
-    # alignment, frames under the stream minimum (bytewise), one and several pieces
-    rnd = random.Random(21)
-    lens = [0, 1, 3, 4, 5, 6, 7, 8, 9, 15, 16, 17, 63, 64, 65, 255, 256, 257, 1500, 1514, 1535, 1536, 1537, 1540,
-            1792, 3072, 3073, 4000, 9000]
-    for L in lens + [rnd.randrange(0, 5000) for _ in range(40)]:
-        for _ in range(3):
-            pre = rnd.randrange(0, 40)
-            base = 4 * rnd.randrange(4)
-            buf = rnd.randbytes(pre + L + 8)
-            assert km.crc32_model_rx(buf, pre, L, base) == zlib.crc32(buf[pre : pre + L]), (L, pre, base)
-    # piece boundaries: one-row and one-dword head pieces at every start alignment
-    for k in (1, 2):
-        for d in range(-6, 9):
-            for pre in range(0, 16, 3):
-                L = 1536 * k + d
-                buf = rnd.randbytes(pre + L + 8)
-                assert km.crc32_model_rx(buf, pre, L, 4 * (pre % 4)) == zlib.crc32(buf[pre : pre + L]), (L, pre)
-
-
-def test_streaming_kernel_geometry():
-    # a 1500-B frame is one piece of 6 rows at every alignment; jumbo frames have full pieces
-    for pre in range(16):
-        assert km.rx_geometry(pre, 1500)[2:] == (1, 6)
-    D, R, npc, h = km.rx_geometry(0, 9000)
-    assert (R, npc, h) == (36, 6, 6)
-    assert km.rx_geometry(0, 64)[2:] == (1, 1)
-    assert km.rx_geometry(3, 4)[2] == 0 and km.rx_geometry(0, 4)[2] == 1

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Diagnostic library builds (wrong results by design; measurement only):
+# Diagnostic library builds (measurement only; the one switch left is -DFS_STAMPS):
 #   tools/build_diag.sh <name> "<-D flags>"  ->  seqs_amd/lib/diag/libframesum_<name>.so
 set -e
 cd "$(dirname "$0")/../seqs_amd/csrc"

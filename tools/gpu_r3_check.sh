@@ -1,0 +1,17 @@
+# Round-3 check: whole GPU suite, smoke(), the driver's bench command, the N>1 gather loop's cost
+# at 20 steps on one GPU (--force-gather against plain), C3.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r3c; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/tests.log | head -20; exit 1; }
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+run() { local name=$1; shift; timeout -k 10 180 "$@" > $O/$name.json 2> $O/$name.err || { echo "FAIL $name"; tail -3 $O/$name.err; exit 1; }; python -c "import json; d=json.loads(open('$O/$name.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$name', d['value'], d['ms_per_step'], r['kernel_avg_us'], r['frac'])"; }
+run driver python bench.py --gpus 1 --steps 20 --warmup 5
+run plain20 python bench.py --steps 20 --warmup 5 --cpu-seconds 0
+run gather20 python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --force-gather
+run plain20b python bench.py --steps 20 --warmup 5 --cpu-seconds 0
+run gather20b python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --force-gather
+run c2_2000 python bench.py --steps 2000 --warmup 500 --cpu-seconds 0
+run c3_1000 python bench.py --config c3 --steps 1000 --warmup 500 --cpu-seconds 0
