@@ -946,9 +946,12 @@ __device__ __forceinline__ void prefetch_unit(const Unit& U, u32x4 (&pf)[kPrefet
     }
 }
 
-// The tables in place. Region A: thread t builds Z64[b][e] (b = t >> 8, e = t & 255) as the XOR
-// of the basis columns of e's set bits and stores its 8 copies (32 contiguous bytes). The plain
-// tables: wave w builds the 1-KB pieces p = w, w + 16, w + 32 (< 40) of the
+// The tables in place. Region A: thread t builds the 16-B chunk k = t & 7 of entry rows
+// e = t >> 3 and e + 128 (the chunk holds 4 of table b = k >> 1's 8 copies of Z64[b][e], the XOR
+// of the basis columns of e's set bits; the two entries differ in bit 7 only). An 8-lane
+// ds_write_b128 group so writes one entry's 128 contiguous bytes: 8 distinct bank quads (one
+// thread per (b, e) writing its 32 B put every lane of a group on the same 4 banks: 8-way).
+// The plain tables: wave w builds the 1-KB pieces p = w, w + 16, w + 32 (< 40) of the
 // 40 [4][256] tables the same way, lane l the entries 4l .. 4l + 3 (one ds_write_b128): no
 // LDS-DMA in the preamble's vector-memory burst, no wait for table pieces at the barrier.
 // The bases come in by scalar loads (lgkmcnt), all issued before one wait, so waiting for them
@@ -961,30 +964,32 @@ __device__ __forceinline__ uint64_t sgpr_addr(const void* p) {
 __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs, char* lds) {
     typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
     const uint32_t t = threadIdx.x;
-    const uint32_t b = __builtin_amdgcn_readfirstlane(t >> 8);  // wave-uniform (64 | 256)
-    const uint32_t e = t & 255u;
-    const uint64_t sa = sgpr_addr(&tabs->z64_basis[b][0]);
-    u32x8 basis;
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint32_t lane = t & 63u;
+    const uint64_t sz = sgpr_addr(&tabs->z64_basis[0][0]);
     const uint64_t s0 = sgpr_addr(&tabs->plain_basis[w][0]);
     const uint64_t s1 = sgpr_addr(&tabs->plain_basis[w + 16u][0]);
     const uint64_t s2 = sgpr_addr(&tabs->plain_basis[min(w + 32u, 39u)][0]);
-    u32x8 pb0, pb1, pb2;
+    u32x8 z0, z1, z2, z3, pb0, pb1, pb2;
     asm volatile(
-        "s_load_dwordx8 %0, %4, 0x0\n\ts_load_dwordx8 %1, %5, 0x0\n\t"
-        "s_load_dwordx8 %2, %6, 0x0\n\ts_load_dwordx8 %3, %7, 0x0\n\ts_waitcnt lgkmcnt(0)"
-        : "=&s"(basis), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
-        : "s"(sa), "s"(s0), "s"(s1), "s"(s2));
-    uint32_t v = 0;
+        "s_load_dwordx8 %0, %7, 0x0\n\ts_load_dwordx8 %1, %7, 0x20\n\ts_load_dwordx8 %2, %7, 0x40\n\t"
+        "s_load_dwordx8 %3, %7, 0x60\n\ts_load_dwordx8 %4, %8, 0x0\n\ts_load_dwordx8 %5, %9, 0x0\n\t"
+        "s_load_dwordx8 %6, %10, 0x0\n\ts_waitcnt lgkmcnt(0)"
+        : "=&s"(z0), "=&s"(z1), "=&s"(z2), "=&s"(z3), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
+        : "s"(sz), "s"(s0), "s"(s1), "s"(s2));
+    const uint32_t k = t & 7u, b = k >> 1, e = t >> 3;  // e < 128
+    uint32_t v = 0, top = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t m = 0u - ((e >> j) & 1u);
-        v ^= basis[j] & m;
+        const uint32_t lo = (b & 1u) ? z1[j] : z0[j];
+        const uint32_t hi = (b & 1u) ? z3[j] : z2[j];
+        const uint32_t bj = (b & 2u) ? hi : lo;
+        if (j < 7) v ^= bj & (0u - ((e >> j) & 1u));
+        else top = bj;
     }
-    u32x4* dst = reinterpret_cast<u32x4*>(lds + kLdsRegionA + e * 256u + 32u * b);
-    dst[0] = u32x4{v, v, v, v};
-    dst[1] = u32x4{v, v, v, v};
+    *reinterpret_cast<u32x4*>(lds + kLdsRegionA + e * 256u + 16u * k) = u32x4{v, v, v, v};
+    v ^= top;
+    *reinterpret_cast<u32x4*>(lds + kLdsRegionA + (e + 128u) * 256u + 16u * k) = u32x4{v, v, v, v};
     auto piece = [&](const u32x8& pb, uint32_t p) {
         uint32_t x = 0;
 #pragma unroll
