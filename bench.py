@@ -13,8 +13,8 @@ batches (> 256 MiB in total) are rotated so the 256 MiB Infinity Cache cannot
 serve them. Multi-GPU (torchrun, one process per GPU, RCCL = torch "nccl"):
 every rank digests its own shard (weak scaling, frame i of the global batch
 on rank i mod N) and the per-frame digests + verdicts go to rank 0 over RCCL in rounds
-(gather_plan: about half the region, at most --gather-every steps; one batch of
-point-to-point transfers per round), overlapped with the next round's kernels; no other
+(gather_plan: each round half of the steps still to come, at most --gather-every; one
+batch of point-to-point transfers per round), overlapped with the later rounds' kernels; no other
 collective. Rank 0 receives the shards as they are (global frame j*N + r is local frame j
 of rank r: seqs_amd.shard.gather_digests shows the interleave; the bench does not spend a
 rank-0 kernel on it). With N > 1 the same line also carries "c4_strong": the C4 strong-scaled
@@ -59,8 +59,8 @@ def parse():
                         "affinity mask); the 1-thread figure is measured beside it")
     p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather (N>1 diagnostics)")
     p.add_argument("--gather-every", type=int, default=64,
-                   help="N>1: at most this many steps per gather round (gather_plan: about half the region, so "
-                        "the region does not end in one transfer of all its slabs)")
+                   help="N>1: at most this many steps per gather round (gather_plan: rounds of half the steps "
+                        "still to come, so the region ends with one step's slabs in flight)")
     p.add_argument("--no-c4", action="store_true", help="N>1: skip the C4 strong-scaled record in the line")
     p.add_argument("--force-gather", action="store_true",
                    help="run the gather path on a single GPU too (a 1-rank process group; a test of the N>1 loop)")
@@ -110,20 +110,33 @@ def with_room(buf, off, ln, room: int = 4):
     return nbuf, noff, ln
 
 
-def gather_plan(steps: int, streams: int, every: int) -> int:
-    """Steps per gather ROUND for a region of `steps` steps: about half the region (at most
-    `every`, at least one step per stream), so the first round goes to rank 0 while the second
-    is still being digested and the region ends with at most half of its slabs in flight."""
-    return max(1, min(max(1, every), max(max(1, streams), (max(1, steps) + 1) // 2)))
+def gather_plan(steps: int, every: int, streams: int = 1) -> list:
+    """The gather ROUNDS of a region of `steps` steps: each round takes half of the steps still
+    to come (at most `every`, at least `streams`), so the rounds shrink toward the end (20 steps
+    over 5 streams: 10, 5, 5). Every round's transfer overlaps the kernels of the rounds after
+    it, and the region ends with at most a round of `streams` steps in flight. (Each round costs
+    the host one event per stream it used: rounds of one step measured 25-30% slower at 20 steps.)"""
+    out, left = [], max(0, steps)
+    lo = max(1, min(streams, every))
+    while left > 0:
+        r = min(max(1, every), max(lo, (left + 1) // 2))
+        if left - r < lo:
+            r = left if left <= every else r  # no round below the floor at the end
+        out.append(r)
+        left -= r
+    return out
 
 
-def gather_schedule(steps: int, R: int):
-    """The gathers one region issues, in issue order: (after_step, buffer, slabs). Step r writes
-    slab r % R of round buffer (r // R) % 2; a round's gather is issued after its last step (or
-    the region's last step), and a buffer is written again only after its previous gather has
-    been waited for. (The step loop below follows exactly this schedule; bench asserts it and
-    tests/test_bench_plan.py checks it.)"""
-    return [(r, (r // R) % 2, r % R + 1) for r in range(steps) if r % R == R - 1 or r == steps - 1]
+def gather_schedule(rounds: list):
+    """The gathers a region issues, in issue order: (after_step, buffer, slabs). Round k writes
+    round buffer k % 2 (slab j = its j-th step) and is sent after its last step; a buffer is
+    written again only after its previous round's transfer has been waited for. (The step loop
+    below follows exactly this schedule; bench asserts it and tests/test_bench_plan.py checks it.)"""
+    out, r0 = [], 0
+    for k, n in enumerate(rounds):
+        out.append((r0 + n - 1, k % 2, n))
+        r0 += n
+    return out
 
 
 def cpu_model() -> str:
@@ -246,12 +259,12 @@ def main():
     # Output slots (digest words, then verdicts, in one 256-B-aligned slab per slot). Without a
     # gather, step i writes slot i % nslot and slot k is only ever written by stream k (nslot ==
     # ns for ns >= 2; one stream for ns == 1): stream order alone keeps a slot's launches apart.
-    # With the gather, the region's steps go in ROUNDS of R consecutive steps (over all streams):
-    # round k's slabs are one contiguous buffer (2 alternate); after its last step the main stream
-    # joins the others and rank 0 receives every other rank's round buffer by one batch of
-    # point-to-point receives (rank r sends its buffer), overlapped with the next round's kernels.
-    # Rank 0's own slabs stay where its kernels wrote them.
-    R = gather_plan(args.steps, ns, args.gather_every) if gather else 1
+    # With the gather, the region's steps go in ROUNDS of consecutive steps (over all streams;
+    # gather_plan: they shrink toward the region's end): round k's slabs are one contiguous
+    # buffer (2 alternate); after its last step a transfer stream waits for every compute stream
+    # and rank 0 receives every other rank's round buffer by one batch of point-to-point
+    # receives (rank r sends its buffer), overlapped with the later rounds' kernels. Rank 0's
+    # own slabs stay where its kernels wrote them.
     nslot = max(2, ns)
     slab = (9 * n + 255) // 256 * 256
 
@@ -259,15 +272,24 @@ def main():
         base = k * slab
         return buf[base : base + 8 * n].view(torch.int32).view(n, 2), buf[base + 8 * n : base + 9 * n]
 
+    def round_map(K):
+        """step r of a K-step region -> (round, slab); the region's rounds (gather_plan)"""
+        rounds = gather_plan(K, args.gather_every, ns)
+        m = [(k, j) for k, c in enumerate(rounds) for j in range(c)]
+        return rounds, m
+
     if gather:
+        plans = {K: round_map(K) for K in {args.steps, args.warmup} if K > 0}
+        R = max(max(p[0]) for p in plans.values())  # slabs per round buffer
         rbuf = [torch.empty(R * slab, dtype=torch.uint8, device=dev) for _ in range(2)]
         rviews = [[views(rbuf[b], j) for j in range(R)] for b in range(2)]
         # rank 0: rank r's round-b slabs at recv[b][r]; 0xFF until received (checked at the end)
         recv = [[torch.full((R * slab,), 0xFF, dtype=torch.uint8, device=dev) for _ in range(world)]
                 for _ in range(2)] if rank == 0 else None
-        pend = [None, None]  # per buffer: the P2P work of its latest gather
+        pend = [None, None]  # per buffer: the P2P work of its latest round
+        xfer = torch.cuda.Stream(dev)  # the rounds' transfers (no compute stream joins another)
         issued = []  # (after_step, buffer, slabs) of the region's gathers (== gather_schedule)
-        last = {}  # buffer -> slabs its latest gather carried
+        last = {}  # buffer -> slabs its latest round carried
     flat = torch.empty(nslot * slab, dtype=torch.uint8, device=dev)
     outs, stats = zip(*[views(flat, k) for k in range(nslot)])
 
@@ -278,21 +300,26 @@ def main():
         if not gather:
             run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=s)
             return
-        b, j = (r // R) % 2, r % R
+        rounds, rmap = plans[K]
+        k, j = rmap[r]
+        b = k % 2
+        # the streams this round's steps run on (its first step is r - j)
+        used = sorted({(r - j + t) % ns for t in range(min(ns, rounds[k]))})
         if j == 0 and pend[b] is not None:
-            # buffer b's previous round has been sent: every stream waits for that (stream-side)
-            for st_ in streams:
-                with torch.cuda.stream(st_):
+            # buffer b's previous round has been sent: the streams that will write it wait for
+            # that (stream-side)
+            for q in used:
+                with torch.cuda.stream(streams[q]):
                     for w in pend[b]:
                         w.wait()
             pend[b] = None
         o, st = rviews[b][j]
         run_op(fb, fo, fl, mtu=0, out=o, status=st, stream=s)
-        if j == R - 1 or r == K - 1:
+        if j == rounds[k] - 1:
             m = j + 1
-            for st_ in streams[1:]:
-                main_stream.wait_stream(st_)
-            with torch.cuda.stream(main_stream):
+            for q in used:
+                xfer.wait_stream(streams[q])
+            with torch.cuda.stream(xfer):
                 if rank == 0:
                     ops = [dist.P2POp(dist.irecv, recv[b][q][: m * slab], q) for q in range(1, world)]
                 else:
@@ -346,7 +373,7 @@ def main():
         elapsed = float(t.item())
 
     if gather:
-        assert issued == gather_schedule(args.steps, R), "the region's gathers differ from gather_schedule"
+        assert issued == gather_schedule(plans[args.steps][0]), "the region's gathers differ from gather_schedule"
     if gather and rank == 0 and world > 1:
         # every other rank's latest round arrived (valid frames: all verdicts 0, where 0xFF was)
         torch.cuda.synchronize()
@@ -491,7 +518,8 @@ def dist_initialized() -> bool:
 def run_c4(args, world, rank, local, dev, frames):
     """C4 (BASELINE configs[3]): one global batch of 1,048,576 x 1500-B frames per step,
     frame i on rank i mod N (strong scaling). A step: every rank digests its shard into a
-    slab (digests + verdicts, fs_shard_slab_bytes layout), RCCL gathers the slabs to rank 0,
+    slab (digests + verdicts, fs_shard_slab_bytes layout), RCCL brings the slabs to rank 0 (one batch
+    of point-to-point transfers into its gather buffer),
     rank 0's de-interleave kernel writes the digests in global frame order. Two slots
     alternate on two streams, so step i's gather and de-interleave overlap step i+1's kernel."""
     import torch
@@ -534,16 +562,23 @@ def run_c4(args, world, rank, local, dev, frames):
         fb, fo, fl = batches[i % nb]
         with torch.cuda.stream(s):
             if pend[k] is not None:
-                pend[k].wait()  # slot k's previous gather has read send[k] (stream-side wait)
+                for w in pend[k]:
+                    w.wait()  # slot k's previous transfer has read send[k] (stream-side wait)
                 pend[k] = None
             o, st = views(k)
             engine.digest_device(fb, fo, fl, mtu=0, out=o, status=st, stream=s)
-            if gather:
-                rl = [recv[k][r * sb : (r + 1) * sb] for r in range(world)] if rank == 0 else None
-                pend[k] = dist.gather(send[k], rl, dst=0, async_op=True)
+            if gather and world > 1:
+                # the gather as one batch of point-to-point transfers straight into rank 0's slab
+                # views (rank 0's own slab is written in place by its kernel)
+                if rank == 0:
+                    ops = [dist.P2POp(dist.irecv, recv[k][r * sb : (r + 1) * sb], r) for r in range(1, world)]
+                else:
+                    ops = [dist.P2POp(dist.isend, send[k], 0)]
+                pend[k] = dist.batch_isend_irecv(ops)
             if rank == 0:
                 if pend[k] is not None:
-                    pend[k].wait()
+                    for w in pend[k]:
+                        w.wait()
                     pend[k] = None
                 engine.deinterleave_device(recv[k], world, n_global, out=gout[k], status=gst[k], stream=s)
 
@@ -551,7 +586,8 @@ def run_c4(args, world, rank, local, dev, frames):
         for k in range(2):
             if pend[k] is not None:
                 with torch.cuda.stream(streams[k]):
-                    pend[k].wait()
+                    for w in pend[k]:
+                        w.wait()
                 pend[k] = None
 
     for i in range(args.warmup):
