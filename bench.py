@@ -41,6 +41,68 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 GIB = float(1 << 30)
 
 
+class GpuOps:
+    """Every device call the bench makes: HIP streams, events and synchronization through
+    torch.cuda, the engine (seqs_amd.Engine over libframesum.so), the process group over RCCL.
+    tests/test_bench_dist.py swaps in CPU stand-ins (and a stand-in engine) to run the bench's
+    own N > 1 loop -- rounds, point-to-point transfers, the C4 record -- over gloo on CPU."""
+
+    backend = "nccl"
+
+    def device(self, local: int):
+        import torch
+
+        torch.cuda.set_device(local)
+        return torch.device("cuda", local)
+
+    def init_group(self, dist, dev, **kw):
+        dist.init_process_group(self.backend, device_id=dev, **kw)
+
+    def stream(self, dev):
+        import torch
+
+        return torch.cuda.Stream(dev)
+
+    def use(self, s):
+        import torch
+
+        return torch.cuda.stream(s)
+
+    def sync(self):
+        import torch
+
+        GPU.sync()
+
+    def event(self):
+        import torch
+
+        return torch.cuda.Event(enable_timing=True)
+
+    def mark(self, s):
+        """an event recorded on stream s now (a dependency marker, no timing)"""
+        import torch
+
+        e = torch.cuda.Event()
+        e.record(s)
+        return e
+
+    def wait_event(self, s, e):
+        s.wait_event(e)
+
+    def empty_cache(self):
+        import torch
+
+        GPU.empty_cache()
+
+    def engine(self, local: int):
+        from seqs_amd import Engine
+
+        return Engine(local)
+
+
+GPU = GpuOps()
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -62,6 +124,8 @@ def parse():
                    help="N>1: at most this many steps per gather round (gather_plan: rounds of half the steps "
                         "still to come, so the region ends with one step's slabs in flight)")
     p.add_argument("--no-c4", action="store_true", help="N>1: skip the C4 strong-scaled record in the line")
+    p.add_argument("--c4-frames", type=int, default=1 << 20,
+                   help="N>1: global frames of the C4 record (BASELINE configs[3]: 1,048,576)")
     p.add_argument("--force-gather", action="store_true",
                    help="run the gather path on a single GPU too (a 1-rank process group; a test of the N>1 loop)")
     p.add_argument("--op", choices=["digest", "fill", "fcs"], default="digest",
@@ -215,23 +279,21 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from seqs_amd import Engine
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = GPU.device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        GPU.init_group(dist, dev)
     elif args.force_gather and not args.no_gather:
-        dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1,
-                                init_method=f"tcp://127.0.0.1:{os.environ.get('MASTER_PORT', '29513')}")
+        GPU.init_group(dist, dev, rank=0, world_size=1,
+                       init_method=f"tcp://127.0.0.1:{os.environ.get('MASTER_PORT', '29513')}")
 
     if args.config == "c4":
         return main_c4(args, world, rank, local, dev)
     n = args.frames or 65536
-    engine = Engine(local)
+    engine = GPU.engine(local)
     engine.set_kernel(args.kernel)
     batches = []
     for b in range(max(1, args.batches)):
@@ -254,8 +316,8 @@ def main():
     # launch there costs about 5 us more, and a short timed region (the driver's 20 steps) pays
     # it on every stream's first launch (tools/sync_overhead.py: 20.5-20.8 against 22.0-22.4 us
     # per step at K = 20; no difference at K = 200)
-    main_stream = torch.cuda.Stream(dev)
-    streams = [main_stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+    main_stream = GPU.stream(dev)
+    streams = [main_stream] + [GPU.stream(dev) for _ in range(ns - 1)]
     # Output slots (digest words, then verdicts, in one 256-B-aligned slab per slot). Without a
     # gather, step i writes slot i % nslot and slot k is only ever written by stream k (nslot ==
     # ns for ns >= 2; one stream for ns == 1): stream order alone keeps a slot's launches apart.
@@ -286,8 +348,8 @@ def main():
         # rank 0: rank r's round-b slabs at recv[b][r]; 0xFF until received (checked at the end)
         recv = [[torch.full((R * slab,), 0xFF, dtype=torch.uint8, device=dev) for _ in range(world)]
                 for _ in range(2)] if rank == 0 else None
-        pend = [None, None]  # per buffer: the P2P work of its latest round
-        xfer = torch.cuda.Stream(dev)  # the rounds' transfers (no compute stream joins another)
+        pend = [None, None]  # per buffer: the event marking its latest round's transfer done
+        xfer = GPU.stream(dev)  # the rounds' transfers (no compute stream joins another)
         issued = []  # (after_step, buffer, slabs) of the region's gathers (== gather_schedule)
         last = {}  # buffer -> slabs its latest round carried
     flat = torch.empty(nslot * slab, dtype=torch.uint8, device=dev)
@@ -307,11 +369,9 @@ def main():
         used = sorted({(r - j + t) % ns for t in range(min(ns, rounds[k]))})
         if j == 0 and pend[b] is not None:
             # buffer b's previous round has been sent: the streams that will write it wait for
-            # that (stream-side)
+            # that round's transfer (its own event, not the transfer stream's later work)
             for q in used:
-                with torch.cuda.stream(streams[q]):
-                    for w in pend[b]:
-                        w.wait()
+                GPU.wait_event(streams[q], pend[b])
             pend[b] = None
         o, st = rviews[b][j]
         run_op(fb, fo, fl, mtu=0, out=o, status=st, stream=s)
@@ -319,12 +379,16 @@ def main():
             m = j + 1
             for q in used:
                 xfer.wait_stream(streams[q])
-            with torch.cuda.stream(xfer):
+            with GPU.use(xfer):
                 if rank == 0:
                     ops = [dist.P2POp(dist.irecv, recv[b][q][: m * slab], q) for q in range(1, world)]
                 else:
                     ops = [dist.P2POp(dist.isend, rbuf[b][: m * slab], 0)]
-                pend[b] = dist.batch_isend_irecv(ops) if ops else []
+                # wait ONCE per work, on the transfer stream (RCCL: a stream-side wait; a second
+                # wait() on a point-to-point work never returns on some backends), and mark it
+                for w in (dist.batch_isend_irecv(ops) if ops else []):
+                    w.wait()
+                pend[b] = GPU.mark(xfer)
             issued.append((r, b, m))
             last[b] = m
 
@@ -333,10 +397,7 @@ def main():
             return
         for b in range(2):
             if pend[b] is not None:
-                for st_ in streams:
-                    with torch.cuda.stream(st_):
-                        for w in pend[b]:
-                            w.wait()
+                GPU.wait_event(main_stream, pend[b])  # (the synchronize after the region covers all)
                 pend[b] = None
 
     # device pre-warm (setup, not steps): throughput settles only after several hundred launches
@@ -346,11 +407,11 @@ def main():
         # over every stream (slot k on stream k): a stream's first launch costs hundreds of us,
         # which must not land in the timed region when --warmup is below the stream count
         run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=streams[i % ns])
-    torch.cuda.synchronize()
+    GPU.sync()
     for i in range(args.warmup):
         step(i, i, args.warmup)
     drain()
-    torch.cuda.synchronize()
+    GPU.sync()
     if gather:
         last.clear()  # the checks below cover the timed region's gathers
         issued.clear()
@@ -358,12 +419,12 @@ def main():
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    GPU.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, i, args.steps)
     drain()
-    torch.cuda.synchronize()
+    GPU.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -376,7 +437,7 @@ def main():
         assert issued == gather_schedule(plans[args.steps][0]), "the region's gathers differ from gather_schedule"
     if gather and rank == 0 and world > 1:
         # every other rank's latest round arrived (valid frames: all verdicts 0, where 0xFF was)
-        torch.cuda.synchronize()
+        GPU.sync()
         for b, m in last.items():
             for q in range(1, world):
                 got = recv[b][q][: m * slab].view(m, slab)[:, 8 * n : 9 * n]
@@ -386,14 +447,14 @@ def main():
     # pair around K back-to-back launches on one stream (no overlap with another launch), so the
     # average is the kernel's duration plus the stream's dispatch gap; an event pair around every
     # launch would add each record's own latency to every launch.
-    k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    with torch.cuda.stream(main_stream):
+    k0, k1 = GPU.event(), GPU.event()
+    with GPU.use(main_stream):
         k0.record(main_stream)
         for i in range(args.steps):  # same stream, in order: no slot events needed
             fb, fo, fl = batches[i % nb]
             run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=main_stream)
         k1.record(main_stream)
-    torch.cuda.synchronize()
+    GPU.sync()
     k_avg_ms = k0.elapsed_time(k1) / args.steps
     engine_last_kernel = engine.last_kernel()
 
@@ -468,8 +529,8 @@ def main():
         del rbuf, rviews, recv
     if world > 1 and args.config == "c2" and args.op == "digest" and not args.no_c4:
         # the C4 strong-scaled record beside the weak-scaled C2 value (same steps / warmup)
-        torch.cuda.empty_cache()
-        c4 = run_c4(args, world, rank, local, dev, frames=1 << 20)
+        GPU.empty_cache()
+        c4 = run_c4(args, world, rank, local, dev, frames=args.c4_frames)
         if rank == 0:
             result["c4_strong"] = {k: c4[k] for k in ("value", "unit", "ms_per_step", "scaling", "config")}
             result["c4_strong"]["kernel_avg_us"] = c4["roofline"]["kernel_avg_us"]
@@ -480,19 +541,19 @@ def main():
     return result
 
 
-def time_region(world, dist, torch, body):
+def time_region(world, dist, torch, body, dev):
     """barrier + synchronize, body(), synchronize + barrier; max over ranks."""
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    GPU.sync()
     t0 = time.perf_counter()
     body()
-    torch.cuda.synchronize()
+    GPU.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -525,10 +586,10 @@ def run_c4(args, world, rank, local, dev, frames):
     import torch
     import torch.distributed as dist
 
-    from seqs_amd import Engine, shard_count, shard_slab_bytes
+    from seqs_amd import shard_count, shard_slab_bytes
 
     n_global = frames
-    engine = Engine(local)
+    engine = GPU.engine(local)
     n = shard_count(n_global, world, rank)
     m = (n_global + world - 1) // world
     sb = shard_slab_bytes(n_global, world)
@@ -543,7 +604,7 @@ def run_c4(args, world, rank, local, dev, frames):
         dist.all_reduce(t)
     bytes_global = int(t.item())
     gather = dist.is_initialized()
-    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]  # created streams (see main())
+    streams = [GPU.stream(dev), GPU.stream(dev)]  # created streams (see main())
     # slot k: rank 0 gathers into recv[k] (world slabs back to back; its own slab is slab 0),
     # other ranks digest into send[k]
     recv = [torch.empty(world * sb, dtype=torch.uint8, device=dev) for _ in range(2)] if rank == 0 else None
@@ -560,7 +621,7 @@ def run_c4(args, world, rank, local, dev, frames):
         k = i % 2
         s = streams[k]
         fb, fo, fl = batches[i % nb]
-        with torch.cuda.stream(s):
+        with GPU.use(s):
             if pend[k] is not None:
                 for w in pend[k]:
                     w.wait()  # slot k's previous transfer has read send[k] (stream-side wait)
@@ -585,7 +646,7 @@ def run_c4(args, world, rank, local, dev, frames):
     def drain():
         for k in range(2):
             if pend[k] is not None:
-                with torch.cuda.stream(streams[k]):
+                with GPU.use(streams[k]):
                     for w in pend[k]:
                         w.wait()
                 pend[k] = None
@@ -593,20 +654,20 @@ def run_c4(args, world, rank, local, dev, frames):
     for i in range(args.warmup):
         step(i)
     drain()
-    torch.cuda.synchronize()
+    GPU.sync()
 
     def body():
         for i in range(args.steps):
             step(args.warmup + i)
         drain()
 
-    elapsed = time_region(world, dist, torch, body)
+    elapsed = time_region(world, dist, torch, body, dev)
 
     # check on rank 0: the last step's global-order output is the interleave of the slabs
     # gathered for it (the de-interleave and the gather layout), and rank 0's own frames
     if rank == 0:
         k = (args.warmup + args.steps - 1) % 2
-        torch.cuda.synchronize()
+        GPU.sync()
         g = recv[k].cpu().numpy()
         i = np.arange(n_global)
         r, j = i % world, i // world
@@ -616,16 +677,16 @@ def run_c4(args, world, rank, local, dev, frames):
         assert (gst[k].cpu().numpy() == 0).all(), "valid frames must all verify"
 
     # kernel-only: K back-to-back shard digests on one stream (events on the launch stream)
-    k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    k0, k1 = GPU.event(), GPU.event()
     ms = streams[0]
-    with torch.cuda.stream(ms):
+    with GPU.use(ms):
         k0.record(ms)
         for i in range(args.steps):
             fb, fo, fl = batches[i % nb]
             o, st = views(0)
             engine.digest_device(fb, fo, fl, mtu=0, out=o, status=st, stream=ms)
         k1.record(ms)
-    torch.cuda.synchronize()
+    GPU.sync()
     k_ms = k0.elapsed_time(k1) / args.steps
     t = torch.tensor([k_ms], dtype=torch.float64, device=dev)
     if world > 1:
