@@ -71,7 +71,7 @@ class GpuOps:
     def sync(self):
         import torch
 
-        GPU.sync()
+        torch.cuda.synchronize()
 
     def event(self):
         import torch
@@ -92,7 +92,7 @@ class GpuOps:
     def empty_cache(self):
         import torch
 
-        GPU.empty_cache()
+        torch.cuda.empty_cache()
 
     def engine(self, local: int):
         from seqs_amd import Engine

@@ -9,6 +9,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
 
 
 def _free_port() -> int:
@@ -55,3 +56,18 @@ def test_long_region_rounds():
     d = _run(["--gpus", "2", "--steps", "64", "--warmup", "7", "--frames", "256", "--no-c4", "--cpu-seconds", "0",
               "--min-warm", "0"])
     assert d["steps"] == 64 and "c4_strong" not in d
+
+
+def test_gpu_seam_calls_torch_cuda():
+    """The real seam (bench.GpuOps) calls torch.cuda / torch.distributed / seqs_amd directly,
+    never back into bench.GPU (the CPU stand-ins above override every method, so the loop
+    tests cannot see that)."""
+    import ast
+    import inspect
+
+    import bench
+
+    src = inspect.getsource(bench.GpuOps)
+    for node in ast.walk(ast.parse(src)):
+        if isinstance(node, ast.Attribute) and isinstance(node.value, ast.Name):
+            assert node.value.id != "GPU", f"GpuOps calls GPU.{node.attr}"
