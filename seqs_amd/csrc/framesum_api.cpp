@@ -54,7 +54,7 @@ struct fs_ctx {
     volatile uint32_t* h_report = nullptr;
     uint32_t* d_report = nullptr;
     int force_kernel = 0;  // fs_ctx_set_kernel
-    uint32_t next_launch_id = 1;  // the ids this context's launches report under (launch_digest)
+    uint32_t next_launch_id = 1;  // the context's launch sequence (launch_digest: report ids, sticky window)
     HostSlot slot[kHostSlots];
     hipStream_t copy_stream = nullptr, compute_stream = nullptr;
     hipStream_t copy_stream2 = nullptr;  // the odd chunks' frame copies
@@ -210,6 +210,8 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
             ctx->h_report[framesum::kReportLatest] = 0u;
             ctx->h_report[framesum::kReportInitial] = framesum::kInitialMixedLaunches;
             ctx->h_report[framesum::kReportChosen] = 0u;
+            ctx->h_report[framesum::kReportSeen] = 0u;
+            ctx->h_report[framesum::kReportSeenSeq] = 0u;
             e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_report), hp, 0);
         }
     }

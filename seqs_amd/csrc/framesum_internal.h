@@ -54,7 +54,9 @@ enum class FsOp { kDigest, kFill, kFcs };
 // The context's host-mapped report block (64 B): word kReportLatest is written by the device (the
 // latest launch id that met mixed-length tiles); the others only by the host: the launches left in
 // the context's initial mixed-kernel window, and the variant of its latest launch.
-constexpr int kReportLatest = 0, kReportInitial = 1, kReportChosen = 2;
+// kReportSeen / kReportSeenSeq (host-only): the report word's value as the host last saw it
+// change, and the context's launch sequence at that moment (the sticky window's clock).
+constexpr int kReportLatest = 0, kReportInitial = 1, kReportChosen = 2, kReportSeen = 3, kReportSeenSeq = 4;
 constexpr uint32_t kInitialMixedLaunches = 16;
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,

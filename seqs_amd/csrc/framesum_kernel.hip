@@ -1625,18 +1625,27 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     // mixed kernel stays chosen for kStickyLaunches launches after the latest report (it keeps
     // reporting while the traffic is mixed). A heuristic only: never a result.
     // Launch ids are 16-bit (they travel in the report pointer's top bits; 0 = never reported).
+    // The window is timed on the host instead: `next_id` is the context's 32-bit launch sequence,
+    // and the host notes the sequence at which it first saw the report word change (host-only
+    // words kReportSeen / kReportSeenSeq), so a report stays recent for kStickyLaunches of this
+    // context's launches and never aliases an old one after the 16-bit ids wrap.
     constexpr uint32_t kStickyLaunches = 4096;
     // (the counter is the context's: another context's launches never shift this one's window;
     // a context is used from one thread at a time, include/framesum.h)
-    uint32_t id = (*next_id)++ & 0xFFFFu;
-    if (id == 0u) id = (*next_id)++ & 0xFFFFu;
+    const uint32_t seq = (*next_id)++;
+    uint32_t id = seq & 0xFFFFu;
+    if (id == 0u) id = 0x8000u;  // (0 means "never reported"; any non-zero tag will do)
     const uint64_t rdev = reinterpret_cast<uint64_t>(report_dev);
     const bool can_report = report_host && rdev != 0u && (rdev >> 48) == 0u;
     const uint64_t report = can_report ? rdev | ((uint64_t)id << 48) : 0u;
     bool mixed = false;
     if (can_report) {
         const uint32_t latest = report_host[kReportLatest];
-        mixed = latest != 0u && ((id - latest) & 0xFFFFu) <= kStickyLaunches;
+        if (latest != report_host[kReportSeen]) {
+            report_host[kReportSeen] = latest;
+            report_host[kReportSeenSeq] = seq;
+        }
+        mixed = latest != 0u && seq - report_host[kReportSeenSeq] <= kStickyLaunches;
         // A context's first launches run the mixed-length kernel: it reports its own mode-B tiles,
         // so mixed traffic keeps it from the first batch on (the one-pass kernel's report would
         // arrive launches late, after slow first batches), and uniform traffic moves to the
