@@ -78,6 +78,22 @@ class GpuOps:
 
         return torch.cuda.Event(enable_timing=True)
 
+    def settle(self, streams):
+        """Wait on the host, by polling, until the work queued so far on `streams` has completed:
+        an event per stream, queried until all have passed. The synchronize that closes a timed
+        region then finds nothing left to wait for. HIP's blocking wait wakes the host about
+        25 us after the last kernel ends; polling sees it within a few us (tools/region_ab.py,
+        profiles/round3/region_ab.log: 20-step C2 region 415 -> 391 us)."""
+        import torch
+
+        evs = []
+        for s in streams:
+            e = torch.cuda.Event()
+            e.record(s)
+            evs.append(e)
+        while not all(e.query() for e in evs):
+            pass
+
     def mark(self, s):
         """an event recorded on stream s now (a dependency marker, no timing)"""
         import torch
@@ -407,10 +423,12 @@ def main():
         # over every stream (slot k on stream k): a stream's first launch costs hundreds of us,
         # which must not land in the timed region when --warmup is below the stream count
         run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=streams[i % ns])
+    GPU.settle(streams)
     GPU.sync()
     for i in range(args.warmup):
         step(i, i, args.warmup)
     drain()
+    GPU.settle(streams + ([xfer] if gather else []))
     GPU.sync()
     if gather:
         last.clear()  # the checks below cover the timed region's gathers
@@ -419,11 +437,13 @@ def main():
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks
     if world > 1:
         dist.barrier()
+    host_warm()
     GPU.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, i, args.steps)
     drain()
+    GPU.settle(streams + ([xfer] if gather else []))
     GPU.sync()
     if world > 1:
         dist.barrier()
@@ -541,13 +561,25 @@ def main():
     return result
 
 
-def time_region(world, dist, torch, body, dev):
-    """barrier + synchronize, body(), synchronize + barrier; max over ranks."""
+def host_warm(seconds: float = 3e-3):
+    """Keep the host thread busy for a few ms before a timed region (no device work). A thread
+    that has just slept in a blocking synchronize enqueues the region's first launches slowly:
+    the 20-step C2 region after a 400-launch burst ran 408-461 us without this, 400-418 us
+    with it (tools/region_ab.py --fresh, profiles/round3/region_ab.log)."""
+    t = time.perf_counter()
+    while time.perf_counter() - t < seconds:
+        pass
+
+
+def time_region(world, dist, torch, body, dev, streams=()):
+    """barrier + synchronize, body(), settle + synchronize + barrier; max over ranks."""
     if world > 1:
         dist.barrier()
+    host_warm()
     GPU.sync()
     t0 = time.perf_counter()
     body()
+    GPU.settle(streams)
     GPU.sync()
     if world > 1:
         dist.barrier()
@@ -654,6 +686,7 @@ def run_c4(args, world, rank, local, dev, frames):
     for i in range(args.warmup):
         step(i)
     drain()
+    GPU.settle(streams)
     GPU.sync()
 
     def body():
@@ -661,7 +694,7 @@ def run_c4(args, world, rank, local, dev, frames):
             step(args.warmup + i)
         drain()
 
-    elapsed = time_region(world, dist, torch, body, dev)
+    elapsed = time_region(world, dist, torch, body, dev, streams)
 
     # check on rank 0: the last step's global-order output is the interleave of the slabs
     # gathered for it (the de-interleave and the gather layout), and rank 0's own frames

@@ -91,6 +91,9 @@ class CpuOps(bench.GpuOps):
     def empty_cache(self):
         pass
 
+    def settle(self, streams):
+        pass
+
     def mark(self, s):
         return None
 
