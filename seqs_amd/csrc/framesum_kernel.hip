@@ -560,7 +560,7 @@ template <uint32_t kOps, class L = LayoutA>
 __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, uint64_t S, uint32_t len,
                                              uint32_t te, uint32_t Y, uint32_t cs, const uint8_t* frames,
                                              uint8_t* wframes, const uint32_t* lengths, uint32_t fi, uint2* out,
-                                             uint8_t* status, uint32_t tx) {
+                                             uint8_t* status, uint32_t tx, uint32_t zinit = 0u) {
     uint32_t fcs = 0u;
     if (kOps == kOpsFcs) {  // the FCS bytes [len, len+4): issued first, used last
         const uint8_t* fp = frames + S + len;
@@ -577,7 +577,8 @@ __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, u
         crcv = ~c;
     } else {
         const uint32_t tpad = (4u - te) & 3u;  // zero bytes appended by the dword rounding
-        crcv = ~L::fin(lds, Y, tpad);
+        // (zinit: the CRC init's contribution Z_len(~0) when the rows streamed a zero-init CRC)
+        crcv = ~(L::fin(lds, Y, tpad) ^ zinit);
     }
     uint32_t verdict = P.verdict, l4 = 0u;
     if (P.compute) l4 = finish_l4(fbs, sa, len, P, cs, verdict);
@@ -1588,23 +1589,482 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 
 
 // =======================================================================================
-// The 16-lane kernel (digest_kernel_w).
+// The WIDE one-pass kernel (digest_kernel_w): the one-pass kernel's tiles of
+// 16 frames, LOADED 16 lanes per frame.
 //
-// A wave owns a SUPER-TILE of 16 consecutive frames (8 or 4 for small batches). The header
-// DMA, the parse and the finish work on it as the 4-lane kernels do (4 lanes per frame). The
-// rows stream in PASSES of 4 frames with a GROUP of 16 lanes per frame: 256-byte rows
-// anchored at the frame's dword-rounded end, lane j of the group loading dwords [4j, 4j+4)
-// of every row (16 B/lane, a 256-B contiguous piece per frame per load instruction -- the
-// access pattern that reads at the plain-stream rate, tools/tile_pattern.hip). The frames are
-// ordered by row count into the passes, so a pass holds frames of similar length. Each lane
-// keeps 4 dword streams with A <- Z256(A) ^ w (region A holds Z_256); a pass ends with the
-// 64-stream combine of each frame (Z12/Z8/Z4 within a lane, Z48/Z32/Z16 within a quad of
-// lanes, Z192/Z128/Z64 across the quads), parked per frame in LDS for the finish.
-// One ring of kPfW row loads runs through the whole launch: a pass's last block refills the
-// ring with the next pass's (or the next super-tile's) first rows, so the loads never drain
-// between passes. The next super-tile's descriptors are loaded one super-tile ahead, its
-// geometry (ordering, rows per pass) and header DMA are set up at the current super-tile's
-// last block.
+// The 4-lane kernels keep 16 frames of a wave streaming at once, each 64 B per load
+// instruction; the memory system reads that pattern 2.2 us slower per C2 launch than a plain
+// stream, and 4 frames x 256 B per instruction at its speed (tools/tile_pattern.hip: the number
+// of frames a wave streams at once is what costs, not the bytes per instruction). So a tile's
+// 16 frames stream as 4 SUB-TILES of 4 frames, one after the other, one ring running through
+// them; lane L streams frame 4s + (L >> 4) of sub-tile s, 16-B chunk c = L & 15 of every
+// 256-B row. Rows are anchored at the frame's dword-rounded end (row k of a frame of `rows`
+// rows holds frame dwords nd - 64 (rows - k) + [0, 64)).
+//
+// The per-byte work is the 4-lane kernels': a lane keeps ONE CRC register, A <- Z256(A) ^ H,
+// with H = Z4(Z4(Z4(d0) ^ d1) ^ d2) ^ d3 the pending register of its chunk (16 lookups per
+// row as before; the 3-deep H chain does not depend on A). Region W holds Z256 and Z4 in the
+// two halves of each 256-B entry row, 8 copies per byte table: the same conflict-free lookup
+// scheme as region A. A sub-tile ends with a 16-lane combine per frame: Y = xor_c
+// Z_16(15 - c)(A_c) by Z64m and Z16a plain tables and a DPP row reduction (the 4-lane kernels'
+// "pending last dword" register), parked in LDS with the checksum partial.
+//
+// Header slots and the parse keep the 4-lane layout ([cell][frame][16 B], frame f = group f of
+// the 4-lane mapping): PHASE 1 streams the first row (two when frame dword 35 lies past it) of
+// all 16 frames at the tile start, masked (head bytes, CRC init), captured into the slots; the
+// parse then runs while the first sub-tile's rows stream (PHASE 2: the rows after them, sub-tile
+// by sub-tile, Q rows per sub-tile, Q a multiple of the ring). The finish runs on the 4-lane
+// mapping from the parked parse and the parked combine.
+constexpr int kRingW = 5;
+// LDS map of the wide kernel: 48 plain [4][256] pieces, region W, header slots, combine slots.
+constexpr uint32_t kWZ16 = 0, kWZ32 = 4096, kWZ48 = 8192, kWZ64 = 12288, kWZ128 = 16384, kWZ192 = 20480,
+                   kWZ12 = 24576, kWZ8 = 28672, kWZfin = 32768;  // Z4 Z3 Z2 Z1 (zfin[t] = Z_(4-t))
+constexpr uint32_t kWRegion = 49152;  // 64 KB: [entry][256 B], Z256 at +0, Z4 at +128
+constexpr uint32_t kWCells = 9;       // slot dwords [0, 36): frame dwords [0, 33) at any dword offset xo <= 3
+constexpr uint32_t kWHdrStride = kWCells * 256u;
+constexpr uint32_t kWHdr = kWRegion + 65536;
+constexpr uint32_t kWScr = kWHdr + kWavesPerBlock * kWHdrStride;  // per wave: 16 frames x {Y, csum}
+constexpr uint32_t kWLdsBytes = kWScr + kWavesPerBlock * 128u;
+static_assert(kWLdsBytes <= kLdsBytes, "the wide kernel's LDS map fits the shared array");
+static_assert(kWRegion + 65536 <= 65536 + 65536, "region W's base folds into the ds_read offset field");
+static_assert(sizeof(((FsTables*)nullptr)->wplain_basis) / 32 == 4 * kWPlainTables, "48 plain pieces");
+
+// Region W and the 48 plain pieces in place, by VALU from their bases (as build_region_a). Wave w
+// builds region W's chunk k = w & 7 of half w >> 3 (table b = k >> 1, copies 4 (k & 1) ..) for
+// entry rows lane + 64 q (its bases: 8 SGPRs), and the plain pieces w, w + 16, w + 32 (SGPRs
+// stay under the budget; the build's 8-lane store groups share a bank quad, which round 3
+// measured not to move the kernel time).
+__device__ __forceinline__ void build_tables_w(const FsTables* __restrict__ tabs, char* lds) {
+    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint32_t lane = t & 63u;
+    const uint32_t k = w & 7u, o = w >> 3, b = k >> 1;
+    const uint64_t sz = sgpr_addr(&tabs->w_basis[o][b][0]);
+    const uint64_t s0 = sgpr_addr(&tabs->wplain_basis[w][0]);
+    const uint64_t s1 = sgpr_addr(&tabs->wplain_basis[w + 16u][0]);
+    const uint64_t s2 = sgpr_addr(&tabs->wplain_basis[w + 32u][0]);
+    u32x8 z, pb0, pb1, pb2;
+    asm volatile(
+        "s_load_dwordx8 %0, %4, 0x0\n\ts_load_dwordx8 %1, %5, 0x0\n\ts_load_dwordx8 %2, %6, 0x0\n\t"
+        "s_load_dwordx8 %3, %7, 0x0\n\ts_waitcnt lgkmcnt(0)"
+        : "=&s"(z), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
+        : "s"(sz), "s"(s0), "s"(s1), "s"(s2));
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 6; ++j) v ^= z[j] & (0u - ((lane >> j) & 1u));
+    char* r0 = lds + kWRegion + 128u * o + 16u * k + lane * 256u;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t x = v ^ ((q & 1u) ? z[6] : 0u) ^ ((q & 2u) ? z[7] : 0u);
+        *reinterpret_cast<u32x4*>(r0 + q * 64u * 256u) = u32x4{x, x, x, x};
+    }
+    auto piece = [&](const u32x8& pb, uint32_t p) {
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
+        const uint32_t x1 = x ^ pb[0];
+        *reinterpret_cast<u32x4*>(lds + 1024u * p + 16u * lane) = u32x4{x, x1, x ^ pb[1], x1 ^ pb[1]};
+    };
+    piece(pb0, w);
+    piece(pb1, w + 16u);
+    piece(pb2, w + 32u);
+}
+
+// One lookup of a replicated region-W operator: Z(a) ^ w (cvec selects the half: Z256 or Z4).
+__device__ __forceinline__ uint32_t zw(const char* lds, uint32_t a, uint32_t cvec, const uint32_t (&sel)[4],
+                                       uint32_t w) {
+    const uint32_t t0 = lds32(lds, kWRegion + __builtin_amdgcn_perm(a, cvec, sel[0]));
+    const uint32_t t1 = lds32(lds, kWRegion + __builtin_amdgcn_perm(a, cvec, sel[1]));
+    const uint32_t t2 = lds32(lds, kWRegion + __builtin_amdgcn_perm(a, cvec, sel[2]));
+    const uint32_t t3 = lds32(lds, kWRegion + __builtin_amdgcn_perm(a, cvec, sel[3]));
+    return xor3(xor3(t0, t1, t2), t3, w);
+}
+struct KeysW {
+    uint32_t cv256, cv4;  // slot bytes (32 b + 4 c) of the Z256 half, and of the Z4 half (+128)
+    uint32_t sel[4];
+};
+// A lane's CRC registers: two dword-pair streams, lo over chunk dwords 0-1 (pending register of
+// dword 1), hi over dwords 2-3 (of dword 3). A row: X <- Z256(X) ^ (Z4(d_even) ^ d_odd) for each,
+// 16 lookups; the Z256 lookups depend only on the register, the Z4 ones only on the data, so a
+// row costs one LDS round trip (a single stream, Z4(Z4(Z4(d0)^d1)^d2)^d3, cost three).
+struct AccW {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ AccW step_w(const char* lds, const KeysW& k, AccW A, uint32_t d0, uint32_t d1,
+                                       uint32_t d2, uint32_t d3) {
+    const uint32_t xl = zw(lds, d0, k.cv4, k.sel, d1), xh = zw(lds, d2, k.cv4, k.sel, d3);
+    return AccW{zw(lds, A.lo, k.cv256, k.sel, xl), zw(lds, A.hi, k.cv256, k.sel, xh)};
+}
+// the first row of a frame (zero registers before it): no Z256 step
+__device__ __forceinline__ AccW first_w(const char* lds, const KeysW& k, uint32_t d0, uint32_t d1, uint32_t d2,
+                                        uint32_t d3) {
+    return AccW{zw(lds, d0, k.cv4, k.sel, d1), zw(lds, d2, k.cv4, k.sel, d3)};
+}
+
+// Z_k(v) for any k from the wide kernel's tables (TX fill): Z256 steps (region W, copy 0),
+// then Z192/Z128/Z64, Z48/Z32/Z16, Z12/Z8/Z4 and Z3/Z2/Z1.
+__device__ __forceinline__ uint32_t zshift_w(const char* lds, uint32_t v, uint32_t k) {
+    for (; k >= 256u; k -= 256u)
+        v = lds32(lds, kWRegion + ((v & 0xffu) << 8)) ^ lds32(lds, kWRegion + (((v >> 8) & 0xffu) << 8) + 32u) ^
+            lds32(lds, kWRegion + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kWRegion + ((v >> 24) << 8) + 96u);
+    const uint32_t m = (k >> 6) & 3u, a = (k >> 4) & 3u, c = (k >> 2) & 3u, t = k & 3u;
+    if (m) v = zplain(lds, v, m == 1u ? kWZ64 : m == 2u ? kWZ128 : kWZ192);
+    if (a) v = zplain(lds, v, a == 1u ? kWZ16 : a == 2u ? kWZ32 : kWZ48);
+    if (c) v = zplain(lds, v, c == 1u ? kWZfin : c == 2u ? kWZ8 : kWZ12);
+    if (t) v = zplain(lds, v, kWZfin + 4096u * (4u - t));
+    return v;
+}
+struct LayoutW {
+    __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift_w(lds, v, k); }
+    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
+        return zplain(lds, v, kWZfin + 4096u * t);
+    }
+    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) { return lds32(lds, kWZfin + 3u * 4096u + (i << 2)); }
+};
+
+// The lane's frame of one sub-tile (from its group's lanes of the 4-lane mapping, by ds_bpermute)
+// and where its loads go: its own frame, or for an empty lane (no frame, or one under 4 bytes)
+// the tile's longest frame, so that every load stays inside a frame.
+struct RowW {
+    const uint32_t* fb;  // dword 0 of the loads' frame
+    int nd, rows;        // own stream dwords and rows (0: nothing to stream)
+    int ndl, rowsl, lo;  // the loads' frame; lo: lowest frame dword a clamped load may start at
+    uint32_t sa, tmask;  // own S & 3; own tail mask
+};
+__device__ __forceinline__ RowW row_state(int s, uint32_t fj, uint64_t S, uint32_t glen, uint64_t SL, int ndL,
+                                          const uint8_t* __restrict__ frames) {
+    RowW R;
+    const int src = (int)((16u * (uint32_t)s + 4u * fj) << 2);
+    const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)S);
+    const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(S >> 32));
+    const uint32_t len = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)glen);
+    R.sa = slo & 3u;
+    R.nd = len >= 4u ? (int)((R.sa + len + 3u) >> 2) : 0;
+    R.rows = (R.nd + 63) >> 6;
+    const uint32_t te = (R.sa + len) & 3u;
+    R.tmask = te ? ((1u << (8u * te)) - 1u) : 0xffffffffu;
+    const uint64_t sdw = R.nd > 0 ? ((((uint64_t)shi << 32) | slo) >> 2) : (SL >> 2);
+    R.ndl = R.nd > 0 ? R.nd : ndL;
+    R.rowsl = (R.ndl + 63) >> 6;
+    R.fb = reinterpret_cast<const uint32_t*>(frames + (sdw << 2));
+    // (as the mixed kernel: never below frames[0]; a frame under 4 dwords loads its last chunk)
+    R.lo = max(sdw > (1u << 24) ? -(1 << 24) : -(int)sdw, min(0, R.ndl - 4));
+    return R;
+}
+
+// Where a sub-tile's row loads go (the part of RowW the ring refills need).
+struct LoadW {
+    const uint32_t* fb;
+    int ndl, lo;
+};
+__device__ __forceinline__ LoadW load_state(const RowW& R) { return LoadW{R.fb, R.ndl, R.lo}; }
+
+template <uint32_t kOps>
+__global__ void __launch_bounds__(kThreads, 1)
+digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+                const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
+                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx,
+                uint32_t fpt) {
+    char* lds = g_lds;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t grp = lane >> 2, gl = lane & 3u;  // 4-lane mapping: header slots, parse, finish
+    const uint32_t fj = lane >> 4, ch = lane & 15u;  // row mapping: frame 4 s + fj of sub-tile s, chunk ch
+    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+    fpt = __builtin_amdgcn_readfirstlane(fpt);
+    const uint32_t ntiles = (n + fpt - 1) / fpt;
+    const uint32_t hw = __builtin_amdgcn_readfirstlane(kWHdr + wave * kWHdrStride);
+    const uint32_t scr = __builtin_amdgcn_readfirstlane(kWScr + wave * 128u);
+    KeysW keys;
+    {
+        const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
+        keys.cv256 = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) keys.cv256 |= (32u * j + 4u * c) << (8u * j);
+        keys.cv4 = keys.cv256 | 0x80808080u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t b = (k + h) & 3u;
+            keys.sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
+        }
+    }
+    uint32_t tile = first_tile(wave);
+#ifdef FS_STAMPS
+    const uint32_t gwave = tile;
+#endif
+    FS_RTSTAMP(5);
+    FS_STAMP(0);
+    uint64_t S;
+    uint32_t len;
+    tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
+    build_tables_w(tabs, lds);
+    FS_STAMP(7);
+    descriptors_ready<kOps>(S, len);
+    FS_STAMP(8);
+    bool barrier_done = false;
+    u32x4 pf[kRingW];
+
+    while (tile < ntiles) {
+        // ---- tile geometry (4-lane mapping: the lane's group's frame)
+        const uint32_t fi = tile * fpt + grp;
+        const bool fvalid = grp < fpt && fi < n;
+        const uint32_t glen = fvalid ? len : 0u;
+        const uint32_t gsa = (uint32_t)S & 3u;
+        const int gnd = glen >= 4u ? (int)((gsa + glen + 3u) >> 2) : 0;
+        const int grows = (gnd + 63) >> 6;
+        // phase 1 streams each frame's first row; phase 2 the rest, Q rows per sub-tile
+        const int Q = (group_max(max(grows - 1, 0)) + kRingW - 1) / kRingW * kRingW;
+        // leading phase-2 rows in which some frame has nothing (yet) to stream, or its CRC init's
+        // second dword (frame dword 1 opens row 1 when nd = 1 mod 64): gated, not lean
+        const int G = group_max(gnd > 0 ? min(max(Q - grows + 1 + ((gnd & 63) == 1 ? 1 : 0), 0), Q) : 0);
+        // the first row holds frame dwords [0, 36) unless it starts at a dword offset below -28:
+        // the header slots' other cells then come by plain loads
+        const bool cap2 = __ballot(gnd > 0 && gnd - 64 * grows < -28) != 0;
+        const int nsub = (int)((min(fpt, n - tile * fpt) + 3u) >> 2);
+        const int Rx = group_max(grows);
+        uint64_t SL = S;
+        int ndL = gnd;
+        {
+            const uint64_t ball = __ballot(grows == Rx);
+            const int src = (int)__builtin_ctzll(ball);
+            SL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(S >> 32), src) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)S, src);
+            ndL = __builtin_amdgcn_readlane(gnd, src);
+        }
+        if (report && mode_b_worthy(gnd) && lane == 0u) post_report(report);
+        const int xo = (-gnd) & 3;  // slot dword of frame dword 0 (cells are 4-aligned in the slot)
+
+        // ---- phase 1: the first row of every frame (loads), and the ring's first block
+        u32x4 ph[4];
+        if (Rx > 0) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (s < nsub) {
+                    const RowW R = row_state(s, fj, S, glen, SL, ndL, frames);
+                    ph[s] = load_row(R.fb, load_pos(R.ndl - 64 * R.rowsl + 4 * (int)ch, R.lo));
+                }
+            }
+        }
+        if (cap2 && grows >= 2) {  // the slot cells past the first row (frames of 2+ rows only)
+            const int cmin = 16 + ((gnd - 64 * grows + xo) >> 2);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int c = (int)gl + 4 * i;
+                if (c < (int)kWCells && c >= cmin) {
+                    const u32x4 v = load_row(reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), 4 * c - xo);
+                    *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)c * 256u + grp * 16u) = v;
+                }
+            }
+        }
+        LoadW lcur = load_state(row_state(0, fj, S, glen, SL, ndL, frames));
+        // phase-2 row t of a sub-tile: frame dword of the lane's chunk
+        auto rel2 = [&](const LoadW& L, int t) { return L.ndl - 64 * (Q - t) + 4 * (int)ch; };
+        if (Q > 0) {  // the ring's first block: sub-tile 0's rows 0 .. kRingW - 1
+            if (G == 0) {
+                const uint32_t* pb = lcur.fb + rel2(lcur, 0);
+#pragma unroll
+                for (int i = 0; i < kRingW; ++i) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + 64 * i);
+            } else {
+#pragma unroll
+                for (int i = 0; i < kRingW; ++i) pf[i] = load_row(lcur.fb, load_pos(rel2(lcur, i), lcur.lo));
+            }
+        }
+        FS_STAMP(9);
+        if (!barrier_done) {
+            // the tables are this wave's own LDS stores (and its permutes): wait for them alone,
+            // then the workgroup's barrier (raw: no vmcnt drain, the rows stay in flight)
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+            if ((__builtin_amdgcn_readfirstlane(wave) >> 3) != 0u) __builtin_amdgcn_s_setprio(1);
+            barrier_done = true;
+        }
+        FS_STAMP(1);
+
+        // a frame's combine: Y = xor_c Z_16(15 - c)(Z8(A_c.lo) ^ A_c.hi) over its 16 lanes (the
+        // pending register of its last dword), the checksum partials summed; parked per frame
+        auto combine = [&](int s, AccW A, uint32_t cs) {
+            const uint32_t sh = 15u - ch, a = sh & 3u, m = sh >> 2;
+            uint32_t v = zplain(lds, A.lo, kWZ8) ^ A.hi;  // the chunk's pending register (of dword 3)
+            const uint32_t v1 = zplain(lds, v, a == 1u ? kWZ16 : a == 2u ? kWZ32 : kWZ48);
+            v = a ? v1 : v;
+            const uint32_t v2 = zplain(lds, v, m == 1u ? kWZ64 : m == 2u ? kWZ128 : kWZ192);
+            v = m ? v2 : v;
+            v ^= dpp_quad<kQuadXor1>(v);
+            v ^= dpp_quad<kQuadXor2>(v);
+            v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+            v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+            uint32_t c = (cs & 0xffffu) + (cs >> 16);
+            c += dpp_quad<kQuadXor1>(c);
+            c += dpp_quad<kQuadXor2>(c);
+            c += (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0x124, 0xf, 0xf, false);
+            c += (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0x128, 0xf, 0xf, false);
+            if (ch == 0u) *reinterpret_cast<uint2*>(lds + scr + 8u * (4u * (uint32_t)s + fj)) = make_uint2(v, c);
+        };
+
+        // ---- phase 1: consume (masked rows: bytes before the frame, head and tail bytes), capture,
+        // and each frame's first-row combine (its registers do not stay live through phase 2: the
+        // finish shifts the parked value past the frame's other rows). The CRC init is not streamed
+        // either: the finish adds its contribution, Z_len(~0).
+        uint32_t tpack = 0u;  // te - 1 of the lane's frame in each sub-tile (2 bits each): the tail masks
+        if (Rx > 0) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (s < nsub) {
+                    const RowW R = row_state(s, fj, S, glen, SL, ndL, frames);
+                    tpack |= (uint32_t)(31 - __builtin_clz(R.tmask | 1u)) / 8u << (2 * s);
+                    const uint32_t f = 4u * (uint32_t)s + fj;  // the frame's group (slot column)
+                    const int rell = R.ndl - 64 * R.rowsl + 4 * (int)ch;
+                    const int sh = load_pos(rell, R.lo) - rell;
+                    const int rel = R.nd - 64 * R.rows + 4 * (int)ch;  // own (== rell when own)
+                    const u32x4 u = ph[s];
+                    uint32_t v[4];
+                    v[0] = u.x;
+                    v[1] = (sh == 0) ? u.y : u.x;
+                    v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
+                    v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
+                    uint32_t d[4], sum = 0u;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int x = rel + j;
+                        uint32_t dd = (x >= 0) ? v[j] : 0u;
+                        if (x == 0) dd &= 0xffffffffu << (8u * R.sa);
+                        if (x == R.nd - 1) dd &= R.tmask;
+                        sum = sad16(dd, sum);
+                        d[j] = dd;
+                    }
+                    const bool upd = R.nd > 0;
+                    const AccW h = first_w(lds, keys, d[0], d[1], d[2], d[3]);
+                    combine(s, AccW{upd ? h.lo : 0u, upd ? h.hi : 0u}, upd ? sum : 0u);
+                    // the header slot: frame dword x at slot dword x + xo (4-aligned here)
+                    const int cell = (rel + ((-R.nd) & 3)) >> 2;
+                    if (upd && cell >= 0 && cell < (int)kWCells)
+                        *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)cell * 256u + f * 16u) =
+                            u32x4{v[0], v[1], v[2], v[3]};
+                }
+            }
+        }
+        FS_STAMP(11);
+        // ---- header parse (4-lane mapping), while the first block of rows is in flight. Then the
+        // parser lanes fold what the finish needs of phase 1 and of the CRC init into one word,
+        // W = Z_te(Z_256(rows-1)(Y1)) ^ Z_len(~0), parked beside the parse with the first row's sum.
+        const bool parser = fvalid && gl == 0u;
+        parse_tile<kOps, kHdrDwords>(hw, grp, gl, gsa, glen, mtu, reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
+                                     parser, hw, (uint32_t)xo);
+        FS_STAMP(12);
+        if (parser && glen >= 4u) {
+            const uint2 y1 = *reinterpret_cast<const uint2*>(lds + scr + 8u * grp);
+            const uint32_t tpad = (4u - ((gsa + glen) & 3u)) & 3u;
+            const uint32_t w = LayoutW::fin(lds, zshift_w(lds, y1.x, 256u * (uint32_t)(grows - 1)), tpad) ^
+                               zshift_w(lds, 0xffffffffu, glen);
+            *reinterpret_cast<uint2*>(lds + hdr_at(hw, grp, 12)) = make_uint2(w, y1.y);
+        }
+
+        FS_STAMP(13);
+        auto tail_of = [&](int s) {
+            const uint32_t te = ((tpack >> (2 * s)) & 3u) + 1u;
+            return (ch == 15u && te < 4u) ? ((1u << (8u * te)) - 1u) : 0xffffffffu;
+        };
+        // A lean block: every row of every lane inside its frame. kRefill: the ring's slots are
+        // refilled from `pb` (the same rows kRingW on, or the next sub-tile's first rows), in place
+        // and never under a branch (a load whose register meets another path is waited for at once).
+        auto lean_block = [&](auto refill_tag, AccW& A, uint32_t& cs, uint32_t tmask_last,
+                              const uint32_t* pb) {
+            constexpr bool kRefill = decltype(refill_tag)::value;
+#pragma unroll
+            for (int i = 0; i < kRingW; ++i) {
+                const u32x4 u = pf[i];
+                const uint32_t d3 = (i == kRingW - 1) ? (u.w & tmask_last) : u.w;
+                A = step_w(lds, keys, A, u.x, u.y, u.z, d3);
+                cs = sad16(d3, sad16(u.z, sad16(u.y, sad16(u.x, cs))));
+                if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + 64 * i);
+                __builtin_amdgcn_sched_barrier(0);  // consume/refill interleaved per row
+            }
+        };
+        using Yes = std::true_type;
+        using No = std::false_type;
+        if (Q > 0 && G == 0) {
+            // ---- phase 2, regular tiles: every row lean. Sub-tiles 0 .. nsub-2, then the last one
+            // (its last block without refill): each loop is one path through the ring's registers.
+            int s = 0;
+            for (; s + 1 < nsub; ++s) {
+                AccW A = {0u, 0u};
+                uint32_t cs = 0u;
+                for (int b = 0; b + kRingW < Q; b += kRingW)
+                    lean_block(Yes(), A, cs, 0xffffffffu, lcur.fb + rel2(lcur, b + kRingW));
+                const LoadW ln = load_state(row_state(s + 1, fj, S, glen, SL, ndL, frames));
+                lean_block(Yes(), A, cs, tail_of(s), ln.fb + rel2(ln, 0));
+                combine(s, A, cs);
+                lcur = ln;
+            }
+            AccW A = {0u, 0u};
+            uint32_t cs = 0u;
+            for (int b = 0; b + kRingW < Q; b += kRingW)
+                lean_block(Yes(), A, cs, 0xffffffffu, lcur.fb + rel2(lcur, b + kRingW));
+            lean_block(No(), A, cs, tail_of(s), lcur.fb);
+            combine(s, A, cs);
+        } else if (Q > 0) {
+            // ---- phase 2, irregular tiles (frames of a sub-tile with different row counts): rows
+            // before a frame's own phase-2 rows leave its registers at zero; clamped refills
+            for (int s = 0; s < nsub; ++s) {
+                AccW A = {0u, 0u};
+                uint32_t cs = 0u;
+                const uint32_t tm = tail_of(s);
+                int tin;
+                {
+                    const RowW R = row_state(s, fj, S, glen, SL, ndL, frames);
+                    tin = R.nd > 0 ? Q - R.rows + 1 : (1 << 20);
+                }
+                LoadW ln = lcur;
+                if (s + 1 < nsub) ln = load_state(row_state(s + 1, fj, S, glen, SL, ndL, frames));
+                for (int b = 0; b < Q; b += kRingW) {
+                    const bool last = b + kRingW >= Q;
+                    const bool refill = !last || s + 1 < nsub;
+                    const LoadW L2 = last ? ln : lcur;
+                    const int t2 = last ? 0 : b + kRingW;
+#pragma unroll
+                    for (int i = 0; i < kRingW; ++i) {
+                        const int t = b + i;
+                        const u32x4 u = pf[i];
+                        const uint32_t d3 = (t == Q - 1) ? (u.w & tm) : u.w;
+                        const AccW An = step_w(lds, keys, A, u.x, u.y, u.z, d3);
+                        const uint32_t sn = sad16(d3, sad16(u.z, sad16(u.y, sad16(u.x, cs))));
+                        A.lo = t >= tin ? An.lo : A.lo;
+                        A.hi = t >= tin ? An.hi : A.hi;
+                        cs = t >= tin ? sn : cs;
+                        const int pos = refill ? load_pos(rel2(L2, t2 + i), L2.lo) : load_pos(rel2(lcur, t), lcur.lo);
+                        pf[i] = load_row(refill ? L2.fb : lcur.fb, pos);  // (a harmless reload without refill)
+                    }
+                }
+                combine(s, A, cs);
+                lcur = ln;
+            }
+        }
+
+        FS_STAMP(2);
+        FS_STAMP(3);
+        // ---- finish (4-lane mapping): the group's lane 0
+        if (parser) {
+            // phase 2's combine (none when no frame has more than one row), phase 1's word
+            const uint2 yc = Q > 0 ? *reinterpret_cast<const uint2*>(lds + scr + 8u * grp) : make_uint2(0u, 0u);
+            const uint32_t te = ((gsa + glen) & 3u) ? ((gsa + glen) & 3u) : 4u;
+            const uint2 w1 = glen >= 4u ? *reinterpret_cast<const uint2*>(lds + hdr_at(hw, grp, 12)) : make_uint2(0u, 0u);
+            finish_frame<kOps, LayoutW>(lds, unpark_parsed<kOps>(lds, hw, grp), S, glen, te, yc.x, yc.y + w1.y,
+                                        frames, wframes, lengths, fi, out, status, tx, w1.x);
+        }
+        FS_STAMP(4);
+        FS_RTSTAMP(6);
+        tile += nwaves;
+        if (tile < ntiles) {
+            tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
+            descriptors_ready<kOps>(S, len);
+        }
+    }
+    if (!barrier_done) {  // a wave without a tile still takes part in the tables barrier
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+    }
+}
 
 }  // namespace
 
@@ -1657,6 +2117,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         }
     }
     if (force) mixed = force == 2;  // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
+    const bool wide = force == 6;   // 6: the wide one-pass kernel (16 lanes per frame)
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {
         if (report_host) report_host[kReportChosen] = v;
@@ -1674,18 +2135,21 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH(K)                                                                                        \
     hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
-    chosen(mixed ? 2u : 4u);
+    chosen(wide ? 6u : mixed ? 2u : 4u);
     switch (op) {
     case FsOp::kDigest:
-        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
+        if (wide) FS_LAUNCH((digest_kernel_w<kOpsDigest>));
+        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
         else FS_LAUNCH((digest_kernel_a<kOpsDigest>));
         break;
     case FsOp::kFill:
-        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
+        if (wide) FS_LAUNCH((digest_kernel_w<kOpsTx>));
+        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
         else FS_LAUNCH((digest_kernel_a<kOpsTx>));
         break;
     case FsOp::kFcs:
-        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
+        if (wide) FS_LAUNCH((digest_kernel_w<kOpsFcs>));
+        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
         else FS_LAUNCH((digest_kernel_a<kOpsFcs>));
         break;
     }

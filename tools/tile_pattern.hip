@@ -28,7 +28,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
         }                                                                                 \
     } while (0)
 
-template <int G, int PF, int AL, int WPB>
+// MAP 0: a wave's tiles are grid-strided (tile gwave + k nwaves); MAP 1: a wave's tiles are
+// consecutive (the wave's share of the batch, 4 consecutive tiles per wave for C2 with G = 16)
+template <int G, int PF, int AL, int WPB, int MAP = 0>
 __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
                                                     uint32_t* out, uint32_t delay_10ns = 0) {
     constexpr int FPT = 64 / G;
@@ -47,7 +49,7 @@ __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ 
     // address of flattened row q for this lane; false if the lane loads nothing
     auto addr = [&](int q, const u32x4_a4*& p) -> bool {
         const int k = q / Rmax, r = q - k * Rmax;
-        const uint32_t f = (gwave + (uint32_t)k * nwaves) * FPT + grp;
+        const uint32_t f = (MAP ? gwave * my_tiles + (uint32_t)k : gwave + (uint32_t)k * nwaves) * FPT + grp;
         if (f >= nframes) return false;
         const uint64_t S = (uint64_t)f * flen, E = S + flen;
         uint64_t a;
@@ -81,6 +83,128 @@ __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ 
             const int qn = q0 + i + PF;
             const u32x4_a4* p;
             if (qn < nq && addr(qn, p)) pf[i] = *p;
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// `burst`: the one-pass kernel's pattern (4 lanes per frame, 64-B block-aligned whole blocks,
+// AL 2) with the ring refilled in BURSTS: H slices of B rows; a slice's B rows are consumed,
+// then re-issued back to back, so each frame's next B blocks (64 B each) reach the memory system
+// together. B = 1 is the per-row refill the kernel uses (ring H rows).
+template <int B, int H, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_burst(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
+                                                    uint32_t* out) {
+    constexpr int G = 4, FPT = 16, PF = B * H;
+    constexpr uint32_t RB = 64u;
+    const uint32_t lane = threadIdx.x & 63u, grp = lane / G, gl = lane % G;
+    const uint32_t gwave = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    const uint32_t nwaves = gridDim.x * WPB;
+    const uint32_t ntiles = (nframes + FPT - 1) / FPT;
+    const uint32_t my_tiles = gwave < ntiles ? (ntiles - gwave + nwaves - 1) / nwaves : 0;
+    const int Rmax = (int)((flen + RB - 1) / RB + 1);
+    const int nq = (int)my_tiles * Rmax;
+    auto addr = [&](int q, const u32x4_a4*& p) -> bool {
+        const int k = q / Rmax, r = q - k * Rmax;
+        const uint32_t f = (gwave + (uint32_t)k * nwaves) * FPT + grp;
+        if (f >= nframes) return false;
+        const uint64_t S = (uint64_t)f * flen, E = S + flen;
+        const uint64_t b0 = S / RB, b1 = (E - 1) / RB;
+        if (b0 + (uint64_t)r > b1) return false;
+        p = reinterpret_cast<const u32x4_a4*>(base + (b0 + r) * RB + 16u * gl);
+        return true;
+    };
+    uint32_t acc = 0;
+    u32x4 pf[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        const u32x4_a4* p;
+        pf[i] = (i < nq && addr(i, p)) ? *p : u32x4{0, 0, 0, 0};
+    }
+    for (int q0 = 0; q0 < nq; q0 += PF) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const u32x4 v = pf[h * B + b];
+                acc = (acc * 3u) ^ v.x ^ v.y ^ v.z ^ v.w;
+            }
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const int qn = q0 + h * B + b + PF;
+                const u32x4_a4* p;
+                if (qn < nq && addr(qn, p)) pf[h * B + b] = *p;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// `super`: 16 frames per wave as the kernel, but LOADED 16 lanes per frame: a super-row is 4
+// blocks (256 B) of each of the 16 frames, 4 load instructions, instruction i covering frames
+// 4i .. 4i+3 (lane L: frame 4i + L/16, block 4r + (L%16)/4 from the frame's first block, chunk
+// L%4; blocks past the frame's last reload it). TR = 1 transposes each super-row through LDS
+// (ds_write_b128 lane-linear, ds_read_b128) into the 4-lanes-per-frame layout the digest
+// kernel computes on (register b, lane 16k + 4j + gl = frame 4k + j, block b, chunk gl).
+// S super-rows in flight.
+template <int S, int TR>
+__global__ void __launch_bounds__(1024) k_super(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
+                                                uint32_t* out) {
+    __shared__ u32x4 stage[16][4][64];
+    constexpr int FPT = 16;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t gwave = wave * gridDim.x + blockIdx.x;
+    const uint32_t nwaves = gridDim.x * 16u;
+    const uint32_t ntiles = (nframes + FPT - 1) / FPT;
+    const uint32_t my_tiles = gwave < ntiles ? (ntiles - gwave + nwaves - 1) / nwaves : 0;
+    const int Rs = (int)(((flen + 63u) / 64u + 1u + 3u) / 4u);  // super-rows per tile (max blocks / 4)
+    const int nq = (int)my_tiles * Rs;
+    const uint32_t fq = lane >> 4, blk = (lane >> 2) & 3u, ch = lane & 3u;
+    auto addr = [&](int q, int i, const u32x4_a4*& p) -> bool {
+        const int k = q / Rs, r = q - k * Rs;
+        const uint32_t f = (gwave + (uint32_t)k * nwaves) * FPT + 4u * (uint32_t)i + fq;
+        if (f >= nframes) return false;
+        const uint64_t S0 = (uint64_t)f * flen, E = S0 + flen;
+        const uint64_t b0 = S0 / 64u, b1 = (E - 1) / 64u;
+        uint64_t b = b0 + 4u * (uint64_t)r + blk;
+        if (b > b1) b = b1;
+        p = reinterpret_cast<const u32x4_a4*>(base + b * 64u + 16u * ch);
+        return true;
+    };
+    uint32_t acc = 0;
+    u32x4 pf[S][4];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4_a4* p;
+            pf[s][i] = (s < nq && addr(s, i, p)) ? *p : u32x4{0, 0, 0, 0};
+        }
+    for (int q0 = 0; q0 < nq; q0 += S) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            if (TR) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) stage[wave][i][lane] = pf[s][i];
+                // R_b at lane 16k + 4j + gl <- X_k at lane 16j + 4b + gl
+                const uint32_t k = lane >> 4, j = (lane >> 2) & 3u, gl = lane & 3u;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const u32x4 v = stage[wave][k][16u * j + 4u * (uint32_t)b + gl];
+                    acc = (acc * 3u) ^ v.x ^ v.y ^ v.z ^ v.w;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc = (acc * 3u) ^ pf[s][i].x ^ pf[s][i].y ^ pf[s][i].z ^ pf[s][i].w;
+            }
+            const int qn = q0 + s + S;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const u32x4_a4* p;
+                if (qn < nq && addr(qn, i, p)) pf[s][i] = *p;
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
     if (acc == 0x12345678u) out[0] = acc;
@@ -193,6 +317,58 @@ int main(int argc, char** argv) {
                 snprintf(nm, sizeof nm, "8 waves, 80 KB, 2 WG/CU, start %u ns", d * 10);
                 ovl(8, 80 * 1024, d, nm);
             }
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "map") {
+#define TILESM(G, PF, AL, MAP)                                                                             \
+    run([&](int i, hipStream_t s) {                                                                       \
+        hipLaunchKernelGGL((k_tiles<G, PF, AL, 16, MAP>), dim3(cus), dim3(1024), 0, s, bufs[i % NB], nf, flen, out); \
+    }, "tiles G=" #G " PF=" #PF " AL=" #AL " MAP=" #MAP)
+        for (int rep = 0; rep < 2; ++rep) {
+            STREAM(4, 16, 1);
+            TILESM(4, 5, 2, 0);
+            TILESM(16, 6, 0, 0);
+            TILESM(16, 6, 0, 1);
+            TILESM(16, 5, 0, 0);
+            TILESM(16, 5, 0, 1);
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "super") {
+#define SUPER(S, TR)                                                                                        \
+    run([&](int i, hipStream_t s) {                                                                       \
+        hipLaunchKernelGGL((k_super<S, TR>), dim3(cus), dim3(1024), 0, s, bufs[i % NB], nf, flen, out); \
+    }, "super S=" #S " TR=" #TR)
+        for (int rep = 0; rep < 2; ++rep) {
+            STREAM(4, 16, 1);
+            TILES(4, 5, 2, 16);
+            TILES(16, 6, false, 16);
+            SUPER(1, 0);
+            SUPER(2, 0);
+            SUPER(3, 0);
+            SUPER(1, 1);
+            SUPER(2, 1);
+            SUPER(3, 1);
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "burst") {
+#define BURST(B, H)                                                                                        \
+    run([&](int i, hipStream_t s) {                                                                       \
+        hipLaunchKernelGGL((k_burst<B, H, 16>), dim3(cus), dim3(1024), 0, s, bufs[i % NB], nf, flen, out); \
+    }, "burst B=" #B " H=" #H " (ring " #B "x" #H ")")
+        for (int rep = 0; rep < 2; ++rep) {
+            STREAM(4, 16, 1);
+            TILES(4, 5, 2, 16);
+            BURST(1, 5);
+            BURST(5, 2);
+            BURST(4, 2);
+            BURST(3, 2);
+            BURST(2, 3);
+            BURST(2, 4);
+            BURST(4, 3);
+            BURST(8, 2);
         }
         return 0;
     }
