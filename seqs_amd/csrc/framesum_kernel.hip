@@ -1615,7 +1615,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 // parse then runs while the first sub-tile's rows stream (PHASE 2: the rows after them, sub-tile
 // by sub-tile, Q rows per sub-tile, Q a multiple of the ring). The finish runs on the 4-lane
 // mapping from the parked parse and the parked combine.
-constexpr int kRingW = 5;
+constexpr int kRingW = 6;
 // LDS map of the wide kernel: 48 plain [4][256] pieces, region W, header slots, combine slots.
 constexpr uint32_t kWZ16 = 0, kWZ32 = 4096, kWZ48 = 8192, kWZ64 = 12288, kWZ128 = 16384, kWZ192 = 20480,
                    kWZ12 = 24576, kWZ8 = 28672, kWZfin = 32768;  // Z4 Z3 Z2 Z1 (zfin[t] = Z_(4-t))
@@ -1629,34 +1629,41 @@ static_assert(kWLdsBytes <= kLdsBytes, "the wide kernel's LDS map fits the share
 static_assert(kWRegion + 65536 <= 65536 + 65536, "region W's base folds into the ds_read offset field");
 static_assert(sizeof(((FsTables*)nullptr)->wplain_basis) / 32 == 4 * kWPlainTables, "48 plain pieces");
 
-// Region W and the 48 plain pieces in place, by VALU from their bases (as build_region_a). Wave w
-// builds region W's chunk k = w & 7 of half w >> 3 (table b = k >> 1, copies 4 (k & 1) ..) for
-// entry rows lane + 64 q (its bases: 8 SGPRs), and the plain pieces w, w + 16, w + 32 (SGPRs
-// stay under the budget; the build's 8-lane store groups share a bank quad, which round 3
-// measured not to move the kernel time).
+// Region W and the 48 plain pieces in place, by VALU from their bases (as build_region_a). Waves
+// 0-7 build the Z256 half, 8-15 the Z4 half: lane l of wave w the chunk k = l & 7 (table k >> 1,
+// copies 4 (k & 1) .. + 3) of entry rows (l >> 3) + 8 (w & 7) + 64 q, so an 8-lane ds_write_b128
+// group writes one entry's 128 contiguous bytes (conflict-free). Wave w also builds the plain
+// pieces w, w + 16, w + 32.
 __device__ __forceinline__ void build_tables_w(const FsTables* __restrict__ tabs, char* lds) {
     typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
     const uint32_t t = threadIdx.x;
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint32_t lane = t & 63u;
-    const uint32_t k = w & 7u, o = w >> 3, b = k >> 1;
-    const uint64_t sz = sgpr_addr(&tabs->w_basis[o][b][0]);
+    const uint32_t o = w >> 3;
+    const uint64_t sz = sgpr_addr(&tabs->w_basis[o][0][0]);
     const uint64_t s0 = sgpr_addr(&tabs->wplain_basis[w][0]);
     const uint64_t s1 = sgpr_addr(&tabs->wplain_basis[w + 16u][0]);
     const uint64_t s2 = sgpr_addr(&tabs->wplain_basis[w + 32u][0]);
-    u32x8 z, pb0, pb1, pb2;
+    u32x8 z0, z1, z2, z3, pb0, pb1, pb2;
     asm volatile(
-        "s_load_dwordx8 %0, %4, 0x0\n\ts_load_dwordx8 %1, %5, 0x0\n\ts_load_dwordx8 %2, %6, 0x0\n\t"
-        "s_load_dwordx8 %3, %7, 0x0\n\ts_waitcnt lgkmcnt(0)"
-        : "=&s"(z), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
+        "s_load_dwordx8 %0, %7, 0x0\n\ts_load_dwordx8 %1, %7, 0x20\n\ts_load_dwordx8 %2, %7, 0x40\n\t"
+        "s_load_dwordx8 %3, %7, 0x60\n\ts_load_dwordx8 %4, %8, 0x0\n\ts_load_dwordx8 %5, %9, 0x0\n\t"
+        "s_load_dwordx8 %6, %10, 0x0\n\ts_waitcnt lgkmcnt(0)"
+        : "=&s"(z0), "=&s"(z1), "=&s"(z2), "=&s"(z3), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
         : "s"(sz), "s"(s0), "s"(s1), "s"(s2));
-    uint32_t v = 0;
+    const uint32_t k = lane & 7u, b = k >> 1, e0 = (lane >> 3) + 8u * (w & 7u);  // e0 < 64
+    uint32_t v = 0, b6 = 0, b7 = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 6; ++j) v ^= z[j] & (0u - ((lane >> j) & 1u));
-    char* r0 = lds + kWRegion + 128u * o + 16u * k + lane * 256u;
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t bj = (b & 2u) ? ((b & 1u) ? z3[j] : z2[j]) : ((b & 1u) ? z1[j] : z0[j]);
+        if (j < 6) v ^= bj & (0u - ((e0 >> j) & 1u));
+        else if (j == 6) b6 = bj;
+        else b7 = bj;
+    }
+    char* r0 = lds + kWRegion + e0 * 256u + 128u * o + 16u * k;
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t x = v ^ ((q & 1u) ? z[6] : 0u) ^ ((q & 2u) ? z[7] : 0u);
+        const uint32_t x = v ^ ((q & 1u) ? b6 : 0u) ^ ((q & 2u) ? b7 : 0u);
         *reinterpret_cast<u32x4*>(r0 + q * 64u * 256u) = u32x4{x, x, x, x};
     }
     auto piece = [&](const u32x8& pb, uint32_t p) {
@@ -1704,10 +1711,12 @@ __device__ __forceinline__ AccW first_w(const char* lds, const KeysW& k, uint32_
 
 // Z_k(v) for any k from the wide kernel's tables (TX fill): Z256 steps (region W, copy 0),
 // then Z192/Z128/Z64, Z48/Z32/Z16, Z12/Z8/Z4 and Z3/Z2/Z1.
-__device__ __forceinline__ uint32_t zshift_w(const char* lds, uint32_t v, uint32_t k) {
+// `cp`: the region-W copy (0..7) the Z256 steps read: lanes with different copies do not share banks
+__device__ __forceinline__ uint32_t zshift_w(const char* lds, uint32_t v, uint32_t k, uint32_t cp = 0u) {
+    const uint32_t c4 = (cp & 7u) << 2;
     for (; k >= 256u; k -= 256u)
-        v = lds32(lds, kWRegion + ((v & 0xffu) << 8)) ^ lds32(lds, kWRegion + (((v >> 8) & 0xffu) << 8) + 32u) ^
-            lds32(lds, kWRegion + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kWRegion + ((v >> 24) << 8) + 96u);
+        v = lds32(lds, kWRegion + c4 + ((v & 0xffu) << 8)) ^ lds32(lds, kWRegion + c4 + (((v >> 8) & 0xffu) << 8) + 32u) ^
+            lds32(lds, kWRegion + c4 + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kWRegion + c4 + ((v >> 24) << 8) + 96u);
     const uint32_t m = (k >> 6) & 3u, a = (k >> 4) & 3u, c = (k >> 2) & 3u, t = k & 3u;
     if (m) v = zplain(lds, v, m == 1u ? kWZ64 : m == 2u ? kWZ128 : kWZ192);
     if (a) v = zplain(lds, v, a == 1u ? kWZ16 : a == 2u ? kWZ32 : kWZ48);
@@ -1749,8 +1758,23 @@ __device__ __forceinline__ RowW row_state(int s, uint32_t fj, uint64_t S, uint32
     R.rowsl = (R.ndl + 63) >> 6;
     R.fb = reinterpret_cast<const uint32_t*>(frames + (sdw << 2));
     // (as the mixed kernel: never below frames[0]; a frame under 4 dwords loads its last chunk)
-    R.lo = max(sdw > (1u << 24) ? -(1 << 24) : -(int)sdw, min(0, R.ndl - 4));
+    // (up to 3 dwords before the frame, so a chunk straddling its start is loaded where it lies;
+    // never below frames[0]; a frame under 4 dwords loads its last chunk)
+    R.lo = max(sdw > (1u << 24) ? -(1 << 24) : -(int)sdw, min(-3, R.ndl - 4));
     return R;
+}
+
+// A row load the compiler does not track (inline asm), and its wait: vmcnt(N) tied to the register,
+// N = the loads issued after it. hipcc's own tracking put a vmcnt(0) in front of the first use of
+// such a load across the tables barrier and the phase-1 branches, which drained the ring with it.
+__device__ __forceinline__ u32x4 load_row_asm(const uint32_t* p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+template <int N>
+__device__ __forceinline__ void wait_row(u32x4& v) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "n"(N));
 }
 
 // Where a sub-tile's row loads go (the part of RowW the ring refills need).
@@ -1768,7 +1792,7 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 uint32_t fpt) {
     char* lds = g_lds;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: scalar tile state)
     const uint32_t grp = lane >> 2, gl = lane & 3u;  // 4-lane mapping: header slots, parse, finish
     const uint32_t fj = lane >> 4, ch = lane & 15u;  // row mapping: frame 4 s + fj of sub-tile s, chunk ch
     const uint32_t nwaves = gridDim.x * kWavesPerBlock;
@@ -1813,15 +1837,6 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         const uint32_t gsa = (uint32_t)S & 3u;
         const int gnd = glen >= 4u ? (int)((gsa + glen + 3u) >> 2) : 0;
         const int grows = (gnd + 63) >> 6;
-        // phase 1 streams each frame's first row; phase 2 the rest, Q rows per sub-tile
-        const int Q = (group_max(max(grows - 1, 0)) + kRingW - 1) / kRingW * kRingW;
-        // leading phase-2 rows in which some frame has nothing (yet) to stream, or its CRC init's
-        // second dword (frame dword 1 opens row 1 when nd = 1 mod 64): gated, not lean
-        const int G = group_max(gnd > 0 ? min(max(Q - grows + 1 + ((gnd & 63) == 1 ? 1 : 0), 0), Q) : 0);
-        // the first row holds frame dwords [0, 36) unless it starts at a dword offset below -28:
-        // the header slots' other cells then come by plain loads
-        const bool cap2 = __ballot(gnd > 0 && gnd - 64 * grows < -28) != 0;
-        const int nsub = (int)((min(fpt, n - tile * fpt) + 3u) >> 2);
         const int Rx = group_max(grows);
         uint64_t SL = S;
         int ndL = gnd;
@@ -1834,42 +1849,33 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         }
         if (report && mode_b_worthy(gnd) && lane == 0u) post_report(report);
         const int xo = (-gnd) & 3;  // slot dword of frame dword 0 (cells are 4-aligned in the slot)
+        // rows per sub-tile: the tile's longest frame, rounded up to whole ring blocks; a REGULAR
+        // tile (every frame that many rows, e.g. all 1500-B frames) masks only each frame's first
+        // row, any other tile masks every row (frames shorter than P have leading rows before them)
+        const int P = (Rx + kRingW - 1) / kRingW * kRingW;
+        const bool regular = Rx > 0 && __ballot(gnd > 0 && grows != P) == 0;
+        // the first row holds frame dwords [0, 36) unless it starts at a dword offset below -28: the
+        // header slot then also takes the second row's cells
+        const bool cap2 = __ballot(gnd > 0 && gnd - 64 * grows < -28) != 0;
+        const int nsub = __builtin_amdgcn_readfirstlane((int)((min(fpt, n - tile * fpt) + 3u) >> 2));
+        if (report && mode_b_worthy(gnd) && lane == 0u) post_report(report);
 
-        // ---- phase 1: the first row of every frame (loads), and the ring's first block
-        u32x4 ph[4];
-        if (Rx > 0) {
+        // row t of a sub-tile: frame dword of the lane's chunk (of the frame its loads read)
+        auto relt = [&](const RowW& R, int t) { return R.ndl - 64 * (P - t) + 4 * (int)ch; };
+        // a row's address, clamped where it starts before the frame (load_pos); the tables when the
+        // tile has nothing to stream (no load sits under a branch: a load whose register meets
+        // another path at a join is waited for at once)
+        auto row_addr = [&](const RowW& R, int t) {
+            const uint32_t* src = R.fb + load_pos(relt(R, t), R.lo);
+            return Rx > 0 ? src : reinterpret_cast<const uint32_t*>(tabs);
+        };
+        // The ring's loads are inline asm with explicit waits (wait_row): every block refills every
+        // slot (the tables stand in for rows past the tile's last), so when slot i is consumed the
+        // other kRingW - 1 slots' loads are the ones issued after it: vmcnt(kRingW - 1), exactly.
+        // hipcc's own tracking lost count across the rows' branches and drained the ring instead.
+        RowW cur = row_state(0, fj, S, glen, SL, ndL, frames);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                if (s < nsub) {
-                    const RowW R = row_state(s, fj, S, glen, SL, ndL, frames);
-                    ph[s] = load_row(R.fb, load_pos(R.ndl - 64 * R.rowsl + 4 * (int)ch, R.lo));
-                }
-            }
-        }
-        if (cap2 && grows >= 2) {  // the slot cells past the first row (frames of 2+ rows only)
-            const int cmin = 16 + ((gnd - 64 * grows + xo) >> 2);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int c = (int)gl + 4 * i;
-                if (c < (int)kWCells && c >= cmin) {
-                    const u32x4 v = load_row(reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), 4 * c - xo);
-                    *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)c * 256u + grp * 16u) = v;
-                }
-            }
-        }
-        LoadW lcur = load_state(row_state(0, fj, S, glen, SL, ndL, frames));
-        // phase-2 row t of a sub-tile: frame dword of the lane's chunk
-        auto rel2 = [&](const LoadW& L, int t) { return L.ndl - 64 * (Q - t) + 4 * (int)ch; };
-        if (Q > 0) {  // the ring's first block: sub-tile 0's rows 0 .. kRingW - 1
-            if (G == 0) {
-                const uint32_t* pb = lcur.fb + rel2(lcur, 0);
-#pragma unroll
-                for (int i = 0; i < kRingW; ++i) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + 64 * i);
-            } else {
-#pragma unroll
-                for (int i = 0; i < kRingW; ++i) pf[i] = load_row(lcur.fb, load_pos(rel2(lcur, i), lcur.lo));
-            }
-        }
+        for (int i = 0; i < kRingW; ++i) pf[i] = load_row_asm(row_addr(cur, i));
         FS_STAMP(9);
         if (!barrier_done) {
             // the tables are this wave's own LDS stores (and its permutes): wait for them alone,
@@ -1901,156 +1907,102 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             c += (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0x128, 0xf, 0xf, false);
             if (ch == 0u) *reinterpret_cast<uint2*>(lds + scr + 8u * (4u * (uint32_t)s + fj)) = make_uint2(v, c);
         };
+        // A masked row of sub-tile s (frame 4 s + fj): the chunk realigned when its load was clamped,
+        // dwords before the frame zeroed, the head and tail bytes masked; the chunk's header-slot
+        // cell written when it holds frame dwords [0, 36). The CRC init is not streamed: the finish
+        // adds its contribution, Z_len(~0).
+        auto masked_row_w = [&](int s, const RowW& R, int t, const u32x4& u, AccW& A, uint32_t& cs) {
+            const int rell = relt(R, t);
+            const int sh = load_pos(rell, R.lo) - rell;
+            const int rel = R.nd - 64 * (P - t) + 4 * (int)ch;  // own (== rell when own)
+            uint32_t v[4] = {u.x, u.y, u.z, u.w};
+            // (a chunk loaded from above its place: only a chunk wholly before its frame -- zeroed
+            // anyway -- or one straddling a frame in the buffer's first 12 bytes)
+            if (__ballot(sh > 0 && sh < 4) != 0) {
+                v[1] = (sh == 0) ? u.y : u.x;
+                v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
+                v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
+            }
+            uint32_t d[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int x = rel + j;
+                uint32_t dd = (R.nd > 0 && x >= 0) ? v[j] : 0u;
+                if (x == 0) dd &= 0xffffffffu << (8u * R.sa);
+                if (x == R.nd - 1) dd &= R.tmask;
+                cs = sad16(dd, cs);
+                d[j] = dd;
+            }
+            A = step_w(lds, keys, A, d[0], d[1], d[2], d[3]);
+            const int cell = (rel + ((-R.nd) & 3)) >> 2;  // frame dword x at slot dword x + xo
+            if (R.nd > 0 && cell >= 0 && cell < (int)kWCells)
+                *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)cell * 256u + (4u * (uint32_t)s + fj) * 16u) =
+                    u32x4{v[0], v[1], v[2], v[3]};
+        };
 
-        // ---- phase 1: consume (masked rows: bytes before the frame, head and tail bytes), capture,
-        // and each frame's first-row combine (its registers do not stay live through phase 2: the
-        // finish shifts the parked value past the frame's other rows). The CRC init is not streamed
-        // either: the finish adds its contribution, Z_len(~0).
-        uint32_t tpack = 0u;  // te - 1 of the lane's frame in each sub-tile (2 bits each): the tail masks
-        if (Rx > 0) {
+        // ---- the rows: sub-tile by sub-tile, P rows each, blocks of kRingW rows; a sub-tile's last
+        // block refills the ring with the next sub-tile's first rows (the tile's last block re-reads
+        // its own: every block refills every slot, so the ring's waits stay exact). A REGULAR tile
+        // (every frame P rows) masks only row 0 (bytes before the frame, head bytes; a chunk
+        // straddling the frame start is loaded where it lies, up to 3 dwords before the frame and
+        // never below frames[0]) and takes the tail mask in its last row's last chunk; any other
+        // tile masks every row and clamps every refill. (The loads are inline asm with explicit
+        // waits, so the uniform branches around them cost no wait.)
+        for (int s = 0; s < nsub; ++s) {
+            const bool more = s + 1 < nsub;
+            RowW nxt = cur;
+            if (more) nxt = row_state(s + 1, fj, S, glen, SL, ndL, frames);
+            const uint32_t tm = ch == 15u ? cur.tmask : 0xffffffffu;
+            AccW A = {0u, 0u};
+            uint32_t cs = 0u;
+            for (int b = 0; b < P; b += kRingW) {
+                const bool last = b + kRingW >= P;
+                const int t2 = last ? 0 : b + kRingW;
+                const uint32_t* tfb = last ? nxt.fb : cur.fb;
+                const int trel = (last ? nxt.ndl : cur.ndl) - 64 * (P - t2) + 4 * (int)ch;
+                const int tlo = last ? nxt.lo : cur.lo;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                if (s < nsub) {
-                    const RowW R = row_state(s, fj, S, glen, SL, ndL, frames);
-                    tpack |= (uint32_t)(31 - __builtin_clz(R.tmask | 1u)) / 8u << (2 * s);
-                    const uint32_t f = 4u * (uint32_t)s + fj;  // the frame's group (slot column)
-                    const int rell = R.ndl - 64 * R.rowsl + 4 * (int)ch;
-                    const int sh = load_pos(rell, R.lo) - rell;
-                    const int rel = R.nd - 64 * R.rows + 4 * (int)ch;  // own (== rell when own)
-                    const u32x4 u = ph[s];
-                    uint32_t v[4];
-                    v[0] = u.x;
-                    v[1] = (sh == 0) ? u.y : u.x;
-                    v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
-                    v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
-                    uint32_t d[4], sum = 0u;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int x = rel + j;
-                        uint32_t dd = (x >= 0) ? v[j] : 0u;
-                        if (x == 0) dd &= 0xffffffffu << (8u * R.sa);
-                        if (x == R.nd - 1) dd &= R.tmask;
-                        sum = sad16(dd, sum);
-                        d[j] = dd;
+                for (int i = 0; i < kRingW; ++i) {
+                    wait_row<kRingW - 1>(pf[i]);
+                    const u32x4 u = pf[i];
+                    if (!regular || (i == 0 && b == 0)) {
+                        masked_row_w(s, cur, b + i, u, A, cs);
+                    } else {
+                        const uint32_t d3 = (i == kRingW - 1 && last) ? (u.w & tm) : u.w;
+                        A = step_w(lds, keys, A, u.x, u.y, u.z, d3);
+                        cs = sad16(d3, sad16(u.z, sad16(u.y, sad16(u.x, cs))));
+                        if (i == 1 && b == 0 && cap2) {  // the second row's header cells
+                            const int rel = cur.nd - 64 * (P - 1) + 4 * (int)ch;
+                            const int cell = (rel + ((-cur.nd) & 3)) >> 2;
+                            if (cur.nd > 0 && cell >= 0 && cell < (int)kWCells)
+                                *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)cell * 256u + (4u * (uint32_t)s + fj) * 16u) = u;
+                        }
                     }
-                    const bool upd = R.nd > 0;
-                    const AccW h = first_w(lds, keys, d[0], d[1], d[2], d[3]);
-                    combine(s, AccW{upd ? h.lo : 0u, upd ? h.hi : 0u}, upd ? sum : 0u);
-                    // the header slot: frame dword x at slot dword x + xo (4-aligned here)
-                    const int cell = (rel + ((-R.nd) & 3)) >> 2;
-                    if (upd && cell >= 0 && cell < (int)kWCells)
-                        *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)cell * 256u + f * 16u) =
-                            u32x4{v[0], v[1], v[2], v[3]};
+                    if (regular && i > 0) pf[i] = load_row_asm(tfb + trel + 64 * i);
+                    else pf[i] = load_row_asm(tfb + load_pos(trel + 64 * i, tlo));
+                    __builtin_amdgcn_sched_barrier(0);  // consume/refill interleaved per row
                 }
             }
+            combine(s, A, cs);
+            cur = nxt;
         }
         FS_STAMP(11);
-        // ---- header parse (4-lane mapping), while the first block of rows is in flight. Then the
-        // parser lanes fold what the finish needs of phase 1 and of the CRC init into one word,
-        // W = Z_te(Z_256(rows-1)(Y1)) ^ Z_len(~0), parked beside the parse with the first row's sum.
+        // ---- header parse (4-lane mapping) and the CRC init's contribution Z_len(~0) (parser lanes)
         const bool parser = fvalid && gl == 0u;
         parse_tile<kOps, kHdrDwords>(hw, grp, gl, gsa, glen, mtu, reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
                                      parser, hw, (uint32_t)xo);
         FS_STAMP(12);
-        if (parser && glen >= 4u) {
-            const uint2 y1 = *reinterpret_cast<const uint2*>(lds + scr + 8u * grp);
-            const uint32_t tpad = (4u - ((gsa + glen) & 3u)) & 3u;
-            const uint32_t w = LayoutW::fin(lds, zshift_w(lds, y1.x, 256u * (uint32_t)(grows - 1)), tpad) ^
-                               zshift_w(lds, 0xffffffffu, glen);
-            *reinterpret_cast<uint2*>(lds + hdr_at(hw, grp, 12)) = make_uint2(w, y1.y);
-        }
-
         FS_STAMP(13);
-        auto tail_of = [&](int s) {
-            const uint32_t te = ((tpack >> (2 * s)) & 3u) + 1u;
-            return (ch == 15u && te < 4u) ? ((1u << (8u * te)) - 1u) : 0xffffffffu;
-        };
-        // A lean block: every row of every lane inside its frame. kRefill: the ring's slots are
-        // refilled from `pb` (the same rows kRingW on, or the next sub-tile's first rows), in place
-        // and never under a branch (a load whose register meets another path is waited for at once).
-        auto lean_block = [&](auto refill_tag, AccW& A, uint32_t& cs, uint32_t tmask_last,
-                              const uint32_t* pb) {
-            constexpr bool kRefill = decltype(refill_tag)::value;
-#pragma unroll
-            for (int i = 0; i < kRingW; ++i) {
-                const u32x4 u = pf[i];
-                const uint32_t d3 = (i == kRingW - 1) ? (u.w & tmask_last) : u.w;
-                A = step_w(lds, keys, A, u.x, u.y, u.z, d3);
-                cs = sad16(d3, sad16(u.z, sad16(u.y, sad16(u.x, cs))));
-                if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + 64 * i);
-                __builtin_amdgcn_sched_barrier(0);  // consume/refill interleaved per row
-            }
-        };
-        using Yes = std::true_type;
-        using No = std::false_type;
-        if (Q > 0 && G == 0) {
-            // ---- phase 2, regular tiles: every row lean. Sub-tiles 0 .. nsub-2, then the last one
-            // (its last block without refill): each loop is one path through the ring's registers.
-            int s = 0;
-            for (; s + 1 < nsub; ++s) {
-                AccW A = {0u, 0u};
-                uint32_t cs = 0u;
-                for (int b = 0; b + kRingW < Q; b += kRingW)
-                    lean_block(Yes(), A, cs, 0xffffffffu, lcur.fb + rel2(lcur, b + kRingW));
-                const LoadW ln = load_state(row_state(s + 1, fj, S, glen, SL, ndL, frames));
-                lean_block(Yes(), A, cs, tail_of(s), ln.fb + rel2(ln, 0));
-                combine(s, A, cs);
-                lcur = ln;
-            }
-            AccW A = {0u, 0u};
-            uint32_t cs = 0u;
-            for (int b = 0; b + kRingW < Q; b += kRingW)
-                lean_block(Yes(), A, cs, 0xffffffffu, lcur.fb + rel2(lcur, b + kRingW));
-            lean_block(No(), A, cs, tail_of(s), lcur.fb);
-            combine(s, A, cs);
-        } else if (Q > 0) {
-            // ---- phase 2, irregular tiles (frames of a sub-tile with different row counts): rows
-            // before a frame's own phase-2 rows leave its registers at zero; clamped refills
-            for (int s = 0; s < nsub; ++s) {
-                AccW A = {0u, 0u};
-                uint32_t cs = 0u;
-                const uint32_t tm = tail_of(s);
-                int tin;
-                {
-                    const RowW R = row_state(s, fj, S, glen, SL, ndL, frames);
-                    tin = R.nd > 0 ? Q - R.rows + 1 : (1 << 20);
-                }
-                LoadW ln = lcur;
-                if (s + 1 < nsub) ln = load_state(row_state(s + 1, fj, S, glen, SL, ndL, frames));
-                for (int b = 0; b < Q; b += kRingW) {
-                    const bool last = b + kRingW >= Q;
-                    const bool refill = !last || s + 1 < nsub;
-                    const LoadW L2 = last ? ln : lcur;
-                    const int t2 = last ? 0 : b + kRingW;
-#pragma unroll
-                    for (int i = 0; i < kRingW; ++i) {
-                        const int t = b + i;
-                        const u32x4 u = pf[i];
-                        const uint32_t d3 = (t == Q - 1) ? (u.w & tm) : u.w;
-                        const AccW An = step_w(lds, keys, A, u.x, u.y, u.z, d3);
-                        const uint32_t sn = sad16(d3, sad16(u.z, sad16(u.y, sad16(u.x, cs))));
-                        A.lo = t >= tin ? An.lo : A.lo;
-                        A.hi = t >= tin ? An.hi : A.hi;
-                        cs = t >= tin ? sn : cs;
-                        const int pos = refill ? load_pos(rel2(L2, t2 + i), L2.lo) : load_pos(rel2(lcur, t), lcur.lo);
-                        pf[i] = load_row(refill ? L2.fb : lcur.fb, pos);  // (a harmless reload without refill)
-                    }
-                }
-                combine(s, A, cs);
-                lcur = ln;
-            }
-        }
-
         FS_STAMP(2);
         FS_STAMP(3);
         // ---- finish (4-lane mapping): the group's lane 0
         if (parser) {
             // phase 2's combine (none when no frame has more than one row), phase 1's word
-            const uint2 yc = Q > 0 ? *reinterpret_cast<const uint2*>(lds + scr + 8u * grp) : make_uint2(0u, 0u);
+            const uint2 yc = *reinterpret_cast<const uint2*>(lds + scr + 8u * grp);
             const uint32_t te = ((gsa + glen) & 3u) ? ((gsa + glen) & 3u) : 4u;
-            const uint2 w1 = glen >= 4u ? *reinterpret_cast<const uint2*>(lds + hdr_at(hw, grp, 12)) : make_uint2(0u, 0u);
-            finish_frame<kOps, LayoutW>(lds, unpark_parsed<kOps>(lds, hw, grp), S, glen, te, yc.x, yc.y + w1.y,
-                                        frames, wframes, lengths, fi, out, status, tx, w1.x);
+            const uint32_t zinit = glen >= 4u ? zshift_w(lds, 0xffffffffu, glen, grp) : 0u;
+            finish_frame<kOps, LayoutW>(lds, unpark_parsed<kOps>(lds, hw, grp), S, glen, te, yc.x, yc.y, frames,
+                                        wframes, lengths, fi, out, status, tx, zinit);
         }
         FS_STAMP(4);
         FS_RTSTAMP(6);
