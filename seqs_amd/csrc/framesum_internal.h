@@ -32,17 +32,7 @@ struct FsTables {
     // T[b][1 << j] of the 40 plain [4][256] tables above, in LDS-image order (piece p = 4 t + b is the
     // 1-KB piece at LDS byte 1024 p): the kernels build them in place by VALU, as region A
     uint32_t plain_basis[40][8];
-    // --- the wide one-pass kernel's tables (digest_kernel_w, 16 lanes per frame), also built in
-    // place from bases: region W (64 KB, [entry][256 B]) holds Z_256 in bytes 0..127 and Z_4 in
-    // bytes 128..255 of each entry row, 8 copies per byte table (the same conflict-free slot
-    // scheme as region A); w_basis[o][b][j] = Z[b][1 << j] of operator o (0: Z_256, 1: Z_4).
-    uint32_t w_basis[2][4][8];
-    // its 48 plain [4][256] pieces (piece p = 4 t + b, LDS byte 1024 p), tables t in order:
-    // Z16 Z32 Z48 Z64 Z128 Z192 Z12 Z8 Z4 Z3 Z2 Z1 (kWTableBytes)
-    uint32_t wplain_basis[48][8];
 };
-constexpr int kWPlainTables = 12;
-constexpr int kWPlainBytes[kWPlainTables] = {16, 32, 48, 64, 128, 192, 12, 8, 4, 3, 2, 1};
 constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 10;  // the LDS image: everything before z64_basis
 static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout");
 static_assert(offsetof(FsTables, z32) == 65536 && offsetof(FsTables, plain_basis) == kTablesLdsBytes + 128,

@@ -560,7 +560,7 @@ template <uint32_t kOps, class L = LayoutA>
 __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, uint64_t S, uint32_t len,
                                              uint32_t te, uint32_t Y, uint32_t cs, const uint8_t* frames,
                                              uint8_t* wframes, const uint32_t* lengths, uint32_t fi, uint2* out,
-                                             uint8_t* status, uint32_t tx, uint32_t zinit = 0u) {
+                                             uint8_t* status, uint32_t tx) {
     uint32_t fcs = 0u;
     if (kOps == kOpsFcs) {  // the FCS bytes [len, len+4): issued first, used last
         const uint8_t* fp = frames + S + len;
@@ -577,8 +577,7 @@ __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, u
         crcv = ~c;
     } else {
         const uint32_t tpad = (4u - te) & 3u;  // zero bytes appended by the dword rounding
-        // (zinit: the CRC init's contribution Z_len(~0) when the rows streamed a zero-init CRC)
-        crcv = ~(L::fin(lds, Y, tpad) ^ zinit);
+        crcv = ~L::fin(lds, Y, tpad);
     }
     uint32_t verdict = P.verdict, l4 = 0u;
     if (P.compute) l4 = finish_l4(fbs, sa, len, P, cs, verdict);
@@ -1589,434 +1588,23 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 
 
 // =======================================================================================
-// The WIDE one-pass kernel (digest_kernel_w): the one-pass kernel's tiles of
-// 16 frames, LOADED 16 lanes per frame.
+// The 16-lane kernel (digest_kernel_w).
 //
-// The 4-lane kernels keep 16 frames of a wave streaming at once, each 64 B per load
-// instruction; the memory system reads that pattern 2.2 us slower per C2 launch than a plain
-// stream, and 4 frames x 256 B per instruction at its speed (tools/tile_pattern.hip: the number
-// of frames a wave streams at once is what costs, not the bytes per instruction). So a tile's
-// 16 frames stream as 4 SUB-TILES of 4 frames, one after the other, one ring running through
-// them; lane L streams frame 4s + (L >> 4) of sub-tile s, 16-B chunk c = L & 15 of every
-// 256-B row. Rows are anchored at the frame's dword-rounded end (row k of a frame of `rows`
-// rows holds frame dwords nd - 64 (rows - k) + [0, 64)).
-//
-// The per-byte work is the 4-lane kernels': a lane keeps ONE CRC register, A <- Z256(A) ^ H,
-// with H = Z4(Z4(Z4(d0) ^ d1) ^ d2) ^ d3 the pending register of its chunk (16 lookups per
-// row as before; the 3-deep H chain does not depend on A). Region W holds Z256 and Z4 in the
-// two halves of each 256-B entry row, 8 copies per byte table: the same conflict-free lookup
-// scheme as region A. A sub-tile ends with a 16-lane combine per frame: Y = xor_c
-// Z_16(15 - c)(A_c) by Z64m and Z16a plain tables and a DPP row reduction (the 4-lane kernels'
-// "pending last dword" register), parked in LDS with the checksum partial.
-//
-// Header slots and the parse keep the 4-lane layout ([cell][frame][16 B], frame f = group f of
-// the 4-lane mapping): PHASE 1 streams the first row (two when frame dword 35 lies past it) of
-// all 16 frames at the tile start, masked (head bytes, CRC init), captured into the slots; the
-// parse then runs while the first sub-tile's rows stream (PHASE 2: the rows after them, sub-tile
-// by sub-tile, Q rows per sub-tile, Q a multiple of the ring). The finish runs on the 4-lane
-// mapping from the parked parse and the parked combine.
-constexpr int kRingW = 6;
-// LDS map of the wide kernel: 48 plain [4][256] pieces, region W, header slots, combine slots.
-constexpr uint32_t kWZ16 = 0, kWZ32 = 4096, kWZ48 = 8192, kWZ64 = 12288, kWZ128 = 16384, kWZ192 = 20480,
-                   kWZ12 = 24576, kWZ8 = 28672, kWZfin = 32768;  // Z4 Z3 Z2 Z1 (zfin[t] = Z_(4-t))
-constexpr uint32_t kWRegion = 49152;  // 64 KB: [entry][256 B], Z256 at +0, Z4 at +128
-constexpr uint32_t kWCells = 9;       // slot dwords [0, 36): frame dwords [0, 33) at any dword offset xo <= 3
-constexpr uint32_t kWHdrStride = kWCells * 256u;
-constexpr uint32_t kWHdr = kWRegion + 65536;
-constexpr uint32_t kWScr = kWHdr + kWavesPerBlock * kWHdrStride;  // per wave: 16 frames x {Y, csum}
-constexpr uint32_t kWLdsBytes = kWScr + kWavesPerBlock * 128u;
-static_assert(kWLdsBytes <= kLdsBytes, "the wide kernel's LDS map fits the shared array");
-static_assert(kWRegion + 65536 <= 65536 + 65536, "region W's base folds into the ds_read offset field");
-static_assert(sizeof(((FsTables*)nullptr)->wplain_basis) / 32 == 4 * kWPlainTables, "48 plain pieces");
-
-// Region W and the 48 plain pieces in place, by VALU from their bases (as build_region_a). Waves
-// 0-7 build the Z256 half, 8-15 the Z4 half: lane l of wave w the chunk k = l & 7 (table k >> 1,
-// copies 4 (k & 1) .. + 3) of entry rows (l >> 3) + 8 (w & 7) + 64 q, so an 8-lane ds_write_b128
-// group writes one entry's 128 contiguous bytes (conflict-free). Wave w also builds the plain
-// pieces w, w + 16, w + 32.
-__device__ __forceinline__ void build_tables_w(const FsTables* __restrict__ tabs, char* lds) {
-    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-    const uint32_t t = threadIdx.x;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const uint32_t lane = t & 63u;
-    const uint32_t o = w >> 3;
-    const uint64_t sz = sgpr_addr(&tabs->w_basis[o][0][0]);
-    const uint64_t s0 = sgpr_addr(&tabs->wplain_basis[w][0]);
-    const uint64_t s1 = sgpr_addr(&tabs->wplain_basis[w + 16u][0]);
-    const uint64_t s2 = sgpr_addr(&tabs->wplain_basis[w + 32u][0]);
-    u32x8 z0, z1, z2, z3, pb0, pb1, pb2;
-    asm volatile(
-        "s_load_dwordx8 %0, %7, 0x0\n\ts_load_dwordx8 %1, %7, 0x20\n\ts_load_dwordx8 %2, %7, 0x40\n\t"
-        "s_load_dwordx8 %3, %7, 0x60\n\ts_load_dwordx8 %4, %8, 0x0\n\ts_load_dwordx8 %5, %9, 0x0\n\t"
-        "s_load_dwordx8 %6, %10, 0x0\n\ts_waitcnt lgkmcnt(0)"
-        : "=&s"(z0), "=&s"(z1), "=&s"(z2), "=&s"(z3), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
-        : "s"(sz), "s"(s0), "s"(s1), "s"(s2));
-    const uint32_t k = lane & 7u, b = k >> 1, e0 = (lane >> 3) + 8u * (w & 7u);  // e0 < 64
-    uint32_t v = 0, b6 = 0, b7 = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t bj = (b & 2u) ? ((b & 1u) ? z3[j] : z2[j]) : ((b & 1u) ? z1[j] : z0[j]);
-        if (j < 6) v ^= bj & (0u - ((e0 >> j) & 1u));
-        else if (j == 6) b6 = bj;
-        else b7 = bj;
-    }
-    char* r0 = lds + kWRegion + e0 * 256u + 128u * o + 16u * k;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t x = v ^ ((q & 1u) ? b6 : 0u) ^ ((q & 2u) ? b7 : 0u);
-        *reinterpret_cast<u32x4*>(r0 + q * 64u * 256u) = u32x4{x, x, x, x};
-    }
-    auto piece = [&](const u32x8& pb, uint32_t p) {
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
-        const uint32_t x1 = x ^ pb[0];
-        *reinterpret_cast<u32x4*>(lds + 1024u * p + 16u * lane) = u32x4{x, x1, x ^ pb[1], x1 ^ pb[1]};
-    };
-    piece(pb0, w);
-    piece(pb1, w + 16u);
-    piece(pb2, w + 32u);
-}
-
-// One lookup of a replicated region-W operator: Z(a) ^ w (cvec selects the half: Z256 or Z4).
-__device__ __forceinline__ uint32_t zw(const char* lds, uint32_t a, uint32_t cvec, const uint32_t (&sel)[4],
-                                       uint32_t w) {
-    const uint32_t t0 = lds32(lds, kWRegion + __builtin_amdgcn_perm(a, cvec, sel[0]));
-    const uint32_t t1 = lds32(lds, kWRegion + __builtin_amdgcn_perm(a, cvec, sel[1]));
-    const uint32_t t2 = lds32(lds, kWRegion + __builtin_amdgcn_perm(a, cvec, sel[2]));
-    const uint32_t t3 = lds32(lds, kWRegion + __builtin_amdgcn_perm(a, cvec, sel[3]));
-    return xor3(xor3(t0, t1, t2), t3, w);
-}
-struct KeysW {
-    uint32_t cv256, cv4;  // slot bytes (32 b + 4 c) of the Z256 half, and of the Z4 half (+128)
-    uint32_t sel[4];
-};
-// A lane's CRC registers: two dword-pair streams, lo over chunk dwords 0-1 (pending register of
-// dword 1), hi over dwords 2-3 (of dword 3). A row: X <- Z256(X) ^ (Z4(d_even) ^ d_odd) for each,
-// 16 lookups; the Z256 lookups depend only on the register, the Z4 ones only on the data, so a
-// row costs one LDS round trip (a single stream, Z4(Z4(Z4(d0)^d1)^d2)^d3, cost three).
-struct AccW {
-    uint32_t lo, hi;
-};
-__device__ __forceinline__ AccW step_w(const char* lds, const KeysW& k, AccW A, uint32_t d0, uint32_t d1,
-                                       uint32_t d2, uint32_t d3) {
-    const uint32_t xl = zw(lds, d0, k.cv4, k.sel, d1), xh = zw(lds, d2, k.cv4, k.sel, d3);
-    return AccW{zw(lds, A.lo, k.cv256, k.sel, xl), zw(lds, A.hi, k.cv256, k.sel, xh)};
-}
-// the first row of a frame (zero registers before it): no Z256 step
-__device__ __forceinline__ AccW first_w(const char* lds, const KeysW& k, uint32_t d0, uint32_t d1, uint32_t d2,
-                                        uint32_t d3) {
-    return AccW{zw(lds, d0, k.cv4, k.sel, d1), zw(lds, d2, k.cv4, k.sel, d3)};
-}
-
-// Z_k(v) for any k from the wide kernel's tables (TX fill): Z256 steps (region W, copy 0),
-// then Z192/Z128/Z64, Z48/Z32/Z16, Z12/Z8/Z4 and Z3/Z2/Z1.
-// `cp`: the region-W copy (0..7) the Z256 steps read: lanes with different copies do not share banks
-__device__ __forceinline__ uint32_t zshift_w(const char* lds, uint32_t v, uint32_t k, uint32_t cp = 0u) {
-    const uint32_t c4 = (cp & 7u) << 2;
-    for (; k >= 256u; k -= 256u)
-        v = lds32(lds, kWRegion + c4 + ((v & 0xffu) << 8)) ^ lds32(lds, kWRegion + c4 + (((v >> 8) & 0xffu) << 8) + 32u) ^
-            lds32(lds, kWRegion + c4 + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kWRegion + c4 + ((v >> 24) << 8) + 96u);
-    const uint32_t m = (k >> 6) & 3u, a = (k >> 4) & 3u, c = (k >> 2) & 3u, t = k & 3u;
-    if (m) v = zplain(lds, v, m == 1u ? kWZ64 : m == 2u ? kWZ128 : kWZ192);
-    if (a) v = zplain(lds, v, a == 1u ? kWZ16 : a == 2u ? kWZ32 : kWZ48);
-    if (c) v = zplain(lds, v, c == 1u ? kWZfin : c == 2u ? kWZ8 : kWZ12);
-    if (t) v = zplain(lds, v, kWZfin + 4096u * (4u - t));
-    return v;
-}
-struct LayoutW {
-    __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift_w(lds, v, k); }
-    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
-        return zplain(lds, v, kWZfin + 4096u * t);
-    }
-    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) { return lds32(lds, kWZfin + 3u * 4096u + (i << 2)); }
-};
-
-// The lane's frame of one sub-tile (from its group's lanes of the 4-lane mapping, by ds_bpermute)
-// and where its loads go: its own frame, or for an empty lane (no frame, or one under 4 bytes)
-// the tile's longest frame, so that every load stays inside a frame.
-struct RowW {
-    const uint32_t* fb;  // dword 0 of the loads' frame
-    int nd, rows;        // own stream dwords and rows (0: nothing to stream)
-    int ndl, rowsl, lo;  // the loads' frame; lo: lowest frame dword a clamped load may start at
-    uint32_t sa, tmask;  // own S & 3; own tail mask
-};
-__device__ __forceinline__ RowW row_state(int s, uint32_t fj, uint64_t S, uint32_t glen, uint64_t SL, int ndL,
-                                          const uint8_t* __restrict__ frames) {
-    RowW R;
-    const int src = (int)((16u * (uint32_t)s + 4u * fj) << 2);
-    const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)S);
-    const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(S >> 32));
-    const uint32_t len = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)glen);
-    R.sa = slo & 3u;
-    R.nd = len >= 4u ? (int)((R.sa + len + 3u) >> 2) : 0;
-    R.rows = (R.nd + 63) >> 6;
-    const uint32_t te = (R.sa + len) & 3u;
-    R.tmask = te ? ((1u << (8u * te)) - 1u) : 0xffffffffu;
-    const uint64_t sdw = R.nd > 0 ? ((((uint64_t)shi << 32) | slo) >> 2) : (SL >> 2);
-    R.ndl = R.nd > 0 ? R.nd : ndL;
-    R.rowsl = (R.ndl + 63) >> 6;
-    R.fb = reinterpret_cast<const uint32_t*>(frames + (sdw << 2));
-    // (as the mixed kernel: never below frames[0]; a frame under 4 dwords loads its last chunk)
-    // (up to 3 dwords before the frame, so a chunk straddling its start is loaded where it lies;
-    // never below frames[0]; a frame under 4 dwords loads its last chunk)
-    R.lo = max(sdw > (1u << 24) ? -(1 << 24) : -(int)sdw, min(-3, R.ndl - 4));
-    return R;
-}
-
-// A row load the compiler does not track (inline asm), and its wait: vmcnt(N) tied to the register,
-// N = the loads issued after it. hipcc's own tracking put a vmcnt(0) in front of the first use of
-// such a load across the tables barrier and the phase-1 branches, which drained the ring with it.
-__device__ __forceinline__ u32x4 load_row_asm(const uint32_t* p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-template <int N>
-__device__ __forceinline__ void wait_row(u32x4& v) {
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "n"(N));
-}
-
-// Where a sub-tile's row loads go (the part of RowW the ring refills need).
-struct LoadW {
-    const uint32_t* fb;
-    int ndl, lo;
-};
-__device__ __forceinline__ LoadW load_state(const RowW& R) { return LoadW{R.fb, R.ndl, R.lo}; }
-
-template <uint32_t kOps>
-__global__ void __launch_bounds__(kThreads, 1)
-digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
-                const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
-                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx,
-                uint32_t fpt) {
-    char* lds = g_lds;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: scalar tile state)
-    const uint32_t grp = lane >> 2, gl = lane & 3u;  // 4-lane mapping: header slots, parse, finish
-    const uint32_t fj = lane >> 4, ch = lane & 15u;  // row mapping: frame 4 s + fj of sub-tile s, chunk ch
-    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-    fpt = __builtin_amdgcn_readfirstlane(fpt);
-    const uint32_t ntiles = (n + fpt - 1) / fpt;
-    const uint32_t hw = __builtin_amdgcn_readfirstlane(kWHdr + wave * kWHdrStride);
-    const uint32_t scr = __builtin_amdgcn_readfirstlane(kWScr + wave * 128u);
-    KeysW keys;
-    {
-        const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
-        keys.cv256 = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) keys.cv256 |= (32u * j + 4u * c) << (8u * j);
-        keys.cv4 = keys.cv256 | 0x80808080u;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t b = (k + h) & 3u;
-            keys.sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
-        }
-    }
-    uint32_t tile = first_tile(wave);
-#ifdef FS_STAMPS
-    const uint32_t gwave = tile;
-#endif
-    FS_RTSTAMP(5);
-    FS_STAMP(0);
-    uint64_t S;
-    uint32_t len;
-    tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
-    build_tables_w(tabs, lds);
-    FS_STAMP(7);
-    descriptors_ready<kOps>(S, len);
-    FS_STAMP(8);
-    bool barrier_done = false;
-    u32x4 pf[kRingW];
-
-    while (tile < ntiles) {
-        // ---- tile geometry (4-lane mapping: the lane's group's frame)
-        const uint32_t fi = tile * fpt + grp;
-        const bool fvalid = grp < fpt && fi < n;
-        const uint32_t glen = fvalid ? len : 0u;
-        const uint32_t gsa = (uint32_t)S & 3u;
-        const int gnd = glen >= 4u ? (int)((gsa + glen + 3u) >> 2) : 0;
-        const int grows = (gnd + 63) >> 6;
-        const int Rx = group_max(grows);
-        uint64_t SL = S;
-        int ndL = gnd;
-        {
-            const uint64_t ball = __ballot(grows == Rx);
-            const int src = (int)__builtin_ctzll(ball);
-            SL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(S >> 32), src) << 32) |
-                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)S, src);
-            ndL = __builtin_amdgcn_readlane(gnd, src);
-        }
-        if (report && mode_b_worthy(gnd) && lane == 0u) post_report(report);
-        const int xo = (-gnd) & 3;  // slot dword of frame dword 0 (cells are 4-aligned in the slot)
-        // rows per sub-tile: the tile's longest frame, rounded up to whole ring blocks; a REGULAR
-        // tile (every frame that many rows, e.g. all 1500-B frames) masks only each frame's first
-        // row, any other tile masks every row (frames shorter than P have leading rows before them)
-        const int P = (Rx + kRingW - 1) / kRingW * kRingW;
-        const bool regular = Rx > 0 && __ballot(gnd > 0 && grows != P) == 0;
-        // the first row holds frame dwords [0, 36) unless it starts at a dword offset below -28: the
-        // header slot then also takes the second row's cells
-        const bool cap2 = __ballot(gnd > 0 && gnd - 64 * grows < -28) != 0;
-        const int nsub = __builtin_amdgcn_readfirstlane((int)((min(fpt, n - tile * fpt) + 3u) >> 2));
-        if (report && mode_b_worthy(gnd) && lane == 0u) post_report(report);
-
-        // row t of a sub-tile: frame dword of the lane's chunk (of the frame its loads read)
-        auto relt = [&](const RowW& R, int t) { return R.ndl - 64 * (P - t) + 4 * (int)ch; };
-        // a row's address, clamped where it starts before the frame (load_pos); the tables when the
-        // tile has nothing to stream (no load sits under a branch: a load whose register meets
-        // another path at a join is waited for at once)
-        auto row_addr = [&](const RowW& R, int t) {
-            const uint32_t* src = R.fb + load_pos(relt(R, t), R.lo);
-            return Rx > 0 ? src : reinterpret_cast<const uint32_t*>(tabs);
-        };
-        // The ring's loads are inline asm with explicit waits (wait_row): every block refills every
-        // slot (the tables stand in for rows past the tile's last), so when slot i is consumed the
-        // other kRingW - 1 slots' loads are the ones issued after it: vmcnt(kRingW - 1), exactly.
-        // hipcc's own tracking lost count across the rows' branches and drained the ring instead.
-        RowW cur = row_state(0, fj, S, glen, SL, ndL, frames);
-#pragma unroll
-        for (int i = 0; i < kRingW; ++i) pf[i] = load_row_asm(row_addr(cur, i));
-        FS_STAMP(9);
-        if (!barrier_done) {
-            // the tables are this wave's own LDS stores (and its permutes): wait for them alone,
-            // then the workgroup's barrier (raw: no vmcnt drain, the rows stay in flight)
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            __builtin_amdgcn_s_barrier();
-            if ((__builtin_amdgcn_readfirstlane(wave) >> 3) != 0u) __builtin_amdgcn_s_setprio(1);
-            barrier_done = true;
-        }
-        FS_STAMP(1);
-
-        // a frame's combine: Y = xor_c Z_16(15 - c)(Z8(A_c.lo) ^ A_c.hi) over its 16 lanes (the
-        // pending register of its last dword), the checksum partials summed; parked per frame
-        auto combine = [&](int s, AccW A, uint32_t cs) {
-            const uint32_t sh = 15u - ch, a = sh & 3u, m = sh >> 2;
-            uint32_t v = zplain(lds, A.lo, kWZ8) ^ A.hi;  // the chunk's pending register (of dword 3)
-            const uint32_t v1 = zplain(lds, v, a == 1u ? kWZ16 : a == 2u ? kWZ32 : kWZ48);
-            v = a ? v1 : v;
-            const uint32_t v2 = zplain(lds, v, m == 1u ? kWZ64 : m == 2u ? kWZ128 : kWZ192);
-            v = m ? v2 : v;
-            v ^= dpp_quad<kQuadXor1>(v);
-            v ^= dpp_quad<kQuadXor2>(v);
-            v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
-            v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
-            uint32_t c = (cs & 0xffffu) + (cs >> 16);
-            c += dpp_quad<kQuadXor1>(c);
-            c += dpp_quad<kQuadXor2>(c);
-            c += (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0x124, 0xf, 0xf, false);
-            c += (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0x128, 0xf, 0xf, false);
-            if (ch == 0u) *reinterpret_cast<uint2*>(lds + scr + 8u * (4u * (uint32_t)s + fj)) = make_uint2(v, c);
-        };
-        // A masked row of sub-tile s (frame 4 s + fj): the chunk realigned when its load was clamped,
-        // dwords before the frame zeroed, the head and tail bytes masked; the chunk's header-slot
-        // cell written when it holds frame dwords [0, 36). The CRC init is not streamed: the finish
-        // adds its contribution, Z_len(~0).
-        auto masked_row_w = [&](int s, const RowW& R, int t, const u32x4& u, AccW& A, uint32_t& cs) {
-            const int rell = relt(R, t);
-            const int sh = load_pos(rell, R.lo) - rell;
-            const int rel = R.nd - 64 * (P - t) + 4 * (int)ch;  // own (== rell when own)
-            uint32_t v[4] = {u.x, u.y, u.z, u.w};
-            // (a chunk loaded from above its place: only a chunk wholly before its frame -- zeroed
-            // anyway -- or one straddling a frame in the buffer's first 12 bytes)
-            if (__ballot(sh > 0 && sh < 4) != 0) {
-                v[1] = (sh == 0) ? u.y : u.x;
-                v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
-                v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
-            }
-            uint32_t d[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int x = rel + j;
-                uint32_t dd = (R.nd > 0 && x >= 0) ? v[j] : 0u;
-                if (x == 0) dd &= 0xffffffffu << (8u * R.sa);
-                if (x == R.nd - 1) dd &= R.tmask;
-                cs = sad16(dd, cs);
-                d[j] = dd;
-            }
-            A = step_w(lds, keys, A, d[0], d[1], d[2], d[3]);
-            const int cell = (rel + ((-R.nd) & 3)) >> 2;  // frame dword x at slot dword x + xo
-            if (R.nd > 0 && cell >= 0 && cell < (int)kWCells)
-                *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)cell * 256u + (4u * (uint32_t)s + fj) * 16u) =
-                    u32x4{v[0], v[1], v[2], v[3]};
-        };
-
-        // ---- the rows: sub-tile by sub-tile, P rows each, blocks of kRingW rows; a sub-tile's last
-        // block refills the ring with the next sub-tile's first rows (the tile's last block re-reads
-        // its own: every block refills every slot, so the ring's waits stay exact). A REGULAR tile
-        // (every frame P rows) masks only row 0 (bytes before the frame, head bytes; a chunk
-        // straddling the frame start is loaded where it lies, up to 3 dwords before the frame and
-        // never below frames[0]) and takes the tail mask in its last row's last chunk; any other
-        // tile masks every row and clamps every refill. (The loads are inline asm with explicit
-        // waits, so the uniform branches around them cost no wait.)
-        for (int s = 0; s < nsub; ++s) {
-            const bool more = s + 1 < nsub;
-            RowW nxt = cur;
-            if (more) nxt = row_state(s + 1, fj, S, glen, SL, ndL, frames);
-            const uint32_t tm = ch == 15u ? cur.tmask : 0xffffffffu;
-            AccW A = {0u, 0u};
-            uint32_t cs = 0u;
-            for (int b = 0; b < P; b += kRingW) {
-                const bool last = b + kRingW >= P;
-                const int t2 = last ? 0 : b + kRingW;
-                const uint32_t* tfb = last ? nxt.fb : cur.fb;
-                const int trel = (last ? nxt.ndl : cur.ndl) - 64 * (P - t2) + 4 * (int)ch;
-                const int tlo = last ? nxt.lo : cur.lo;
-#pragma unroll
-                for (int i = 0; i < kRingW; ++i) {
-                    wait_row<kRingW - 1>(pf[i]);
-                    const u32x4 u = pf[i];
-                    if (!regular || (i == 0 && b == 0)) {
-                        masked_row_w(s, cur, b + i, u, A, cs);
-                    } else {
-                        const uint32_t d3 = (i == kRingW - 1 && last) ? (u.w & tm) : u.w;
-                        A = step_w(lds, keys, A, u.x, u.y, u.z, d3);
-                        cs = sad16(d3, sad16(u.z, sad16(u.y, sad16(u.x, cs))));
-                        if (i == 1 && b == 0 && cap2) {  // the second row's header cells
-                            const int rel = cur.nd - 64 * (P - 1) + 4 * (int)ch;
-                            const int cell = (rel + ((-cur.nd) & 3)) >> 2;
-                            if (cur.nd > 0 && cell >= 0 && cell < (int)kWCells)
-                                *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)cell * 256u + (4u * (uint32_t)s + fj) * 16u) = u;
-                        }
-                    }
-                    if (regular && i > 0) pf[i] = load_row_asm(tfb + trel + 64 * i);
-                    else pf[i] = load_row_asm(tfb + load_pos(trel + 64 * i, tlo));
-                    __builtin_amdgcn_sched_barrier(0);  // consume/refill interleaved per row
-                }
-            }
-            combine(s, A, cs);
-            cur = nxt;
-        }
-        FS_STAMP(11);
-        // ---- header parse (4-lane mapping) and the CRC init's contribution Z_len(~0) (parser lanes)
-        const bool parser = fvalid && gl == 0u;
-        parse_tile<kOps, kHdrDwords>(hw, grp, gl, gsa, glen, mtu, reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
-                                     parser, hw, (uint32_t)xo);
-        FS_STAMP(12);
-        FS_STAMP(13);
-        FS_STAMP(2);
-        FS_STAMP(3);
-        // ---- finish (4-lane mapping): the group's lane 0
-        if (parser) {
-            // phase 2's combine (none when no frame has more than one row), phase 1's word
-            const uint2 yc = *reinterpret_cast<const uint2*>(lds + scr + 8u * grp);
-            const uint32_t te = ((gsa + glen) & 3u) ? ((gsa + glen) & 3u) : 4u;
-            const uint32_t zinit = glen >= 4u ? zshift_w(lds, 0xffffffffu, glen, grp) : 0u;
-            finish_frame<kOps, LayoutW>(lds, unpark_parsed<kOps>(lds, hw, grp), S, glen, te, yc.x, yc.y, frames,
-                                        wframes, lengths, fi, out, status, tx, zinit);
-        }
-        FS_STAMP(4);
-        FS_RTSTAMP(6);
-        tile += nwaves;
-        if (tile < ntiles) {
-            tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
-            descriptors_ready<kOps>(S, len);
-        }
-    }
-    if (!barrier_done) {  // a wave without a tile still takes part in the tables barrier
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_s_barrier();
-    }
-}
+// A wave owns a SUPER-TILE of 16 consecutive frames (8 or 4 for small batches). The header
+// DMA, the parse and the finish work on it as the 4-lane kernels do (4 lanes per frame). The
+// rows stream in PASSES of 4 frames with a GROUP of 16 lanes per frame: 256-byte rows
+// anchored at the frame's dword-rounded end, lane j of the group loading dwords [4j, 4j+4)
+// of every row (16 B/lane, a 256-B contiguous piece per frame per load instruction -- the
+// access pattern that reads at the plain-stream rate, tools/tile_pattern.hip). The frames are
+// ordered by row count into the passes, so a pass holds frames of similar length. Each lane
+// keeps 4 dword streams with A <- Z256(A) ^ w (region A holds Z_256); a pass ends with the
+// 64-stream combine of each frame (Z12/Z8/Z4 within a lane, Z48/Z32/Z16 within a quad of
+// lanes, Z192/Z128/Z64 across the quads), parked per frame in LDS for the finish.
+// One ring of kPfW row loads runs through the whole launch: a pass's last block refills the
+// ring with the next pass's (or the next super-tile's) first rows, so the loads never drain
+// between passes. The next super-tile's descriptors are loaded one super-tile ahead, its
+// geometry (ordering, rows per pass) and header DMA are set up at the current super-tile's
+// last block.
 
 }  // namespace
 
@@ -2069,7 +1657,6 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         }
     }
     if (force) mixed = force == 2;  // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
-    const bool wide = force == 6;   // 6: the wide one-pass kernel (16 lanes per frame)
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {
         if (report_host) report_host[kReportChosen] = v;
@@ -2087,21 +1674,18 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH(K)                                                                                        \
     hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
-    chosen(wide ? 6u : mixed ? 2u : 4u);
+    chosen(mixed ? 2u : 4u);
     switch (op) {
     case FsOp::kDigest:
-        if (wide) FS_LAUNCH((digest_kernel_w<kOpsDigest>));
-        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
         else FS_LAUNCH((digest_kernel_a<kOpsDigest>));
         break;
     case FsOp::kFill:
-        if (wide) FS_LAUNCH((digest_kernel_w<kOpsTx>));
-        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
         else FS_LAUNCH((digest_kernel_a<kOpsTx>));
         break;
     case FsOp::kFcs:
-        if (wide) FS_LAUNCH((digest_kernel_w<kOpsFcs>));
-        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
         else FS_LAUNCH((digest_kernel_a<kOpsFcs>));
         break;
     }

@@ -71,28 +71,6 @@ void build_tables(FsTables* t) {
                 if ((e >> j) & 1u) v ^= t->plain_basis[p][j];
             if (v != plain[256 * p + e]) throw std::logic_error("plain table basis mismatch");
         }
-    // the wide kernel's bases (digest_kernel_w): region W's two operators and its 48 plain pieces
-    {
-        static uint32_t w[4][256];
-        const int wops[2] = {256, 4};
-        for (int o = 0; o < 2; ++o) {
-            op_table(t1, wops[o], w);
-            for (uint32_t b = 0; b < 4; ++b)
-                for (uint32_t j = 0; j < 8; ++j) t->w_basis[o][b][j] = w[b][1u << j];
-        }
-        for (int tt = 0; tt < kWPlainTables; ++tt) {
-            op_table(t1, kWPlainBytes[tt], w);
-            for (uint32_t b = 0; b < 4; ++b) {
-                for (uint32_t j = 0; j < 8; ++j) t->wplain_basis[4 * tt + b][j] = w[b][1u << j];
-                for (uint32_t e = 0; e < 256; ++e) {
-                    uint32_t v = 0;
-                    for (uint32_t j = 0; j < 8; ++j)
-                        if ((e >> j) & 1u) v ^= t->wplain_basis[4 * tt + b][j];
-                    if (v != w[b][e]) throw std::logic_error("wide plain table basis mismatch");
-                }
-            }
-        }
-    }
     // The final step Z_(4-t) replaces "Z_4 then undo t appended zero bytes"; Z_1[0] is the
     // standard byte table used for frames shorter than 4 bytes.
     if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");

@@ -58,13 +58,7 @@ print(f"  realtime: span {us(re_.max() - t0):.2f} us; wave start offset p50/p90/
       f"wave end p10/p50/p90/max {us(np.percentile(re_ - t0, 10)):.2f}/{us(np.median(re_ - t0)):.2f}/"
       f"{us(np.percentile(re_ - t0, 90)):.2f}/{us((re_ - t0).max()):.2f} us")
 print(f"  memtime ticks per us (median over waves): {np.median((s[:, 4] - s[:, 0]) / np.maximum(1, us(re_ - rs))):.0f}")
-if a.kernel == 6:  # the wide kernel's phases
-    for nm, a_, b_ in (("start->tables", 0, 7), ("tables->desc", 7, 8), ("desc->ring issued", 8, 9),
-                       ("issued->barrier", 9, 1), ("phase 1", 1, 11), ("parse", 11, 12), ("phase-1 word", 12, 13),
-                       ("phase 2", 13, 2), ("finish", 3, 4)):
-        d = s[:, b_] - s[:, a_]
-        print(f"  {nm:18s} median {int(np.median(d)):8d}  p10 {int(np.percentile(d, 10)):8d}  p90 {int(np.percentile(d, 90)):8d}")
-elif s[:, 9].any():
+if s[:, 9].any():
     for nm, a_, b_ in (("start->regionA", 0, 7), ("regionA->desc", 7, 8), ("start->desc (fine)", 0, 8), ("desc->geom+issue", 8, 9), ("start->geom+issue", 0, 9),
                        ("issue->waitcnt", 9, 10), ("waitcnt->barrier", 10, 1),
                        ("desc->geometry", 8, 11), ("geometry->report", 11, 12), ("report->header", 12, 13),
