@@ -425,11 +425,15 @@ def main():
         run_op(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=streams[i % ns])
     GPU.settle(streams)
     GPU.sync()
+    if world > 1:
+        dist.barrier()
+    # the host spin first, then the warmup steps right before the region: the GPU stays busy up
+    # to it (an idle GPU before a 20-step region cost ~9 us, tools/region_ab.py, round 3)
+    host_warm()
     for i in range(args.warmup):
         step(i, i, args.warmup)
     drain()
     GPU.settle(streams + ([xfer] if gather else []))
-    GPU.sync()
     if gather:
         last.clear()  # the checks below cover the timed region's gathers
         issued.clear()
@@ -437,7 +441,6 @@ def main():
     # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks
     if world > 1:
         dist.barrier()
-    host_warm()
     GPU.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -562,10 +565,12 @@ def main():
 
 
 def host_warm(seconds: float = 3e-3):
-    """Keep the host thread busy for a few ms before a timed region (no device work). A thread
-    that has just slept in a blocking synchronize enqueues the region's first launches slowly:
-    the 20-step C2 region after a 400-launch burst ran 408-461 us without this, 400-418 us
-    with it (tools/region_ab.py --fresh, profiles/round3/region_ab.log)."""
+    """Keep the host thread busy for a few ms before the warmup steps that precede a timed region
+    (no device work). A thread that has just slept in a blocking synchronize enqueues the region's
+    first launches slowly: the 20-step C2 region after a 400-launch burst ran 408-461 us without
+    this, 400-418 us with it; spinning before the warmup steps rather than after them (so the GPU
+    is not idle right before the region) ran 398-402 us (tools/region_ab.py --fresh,
+    profiles/round3/region_ab.log)."""
     t = time.perf_counter()
     while time.perf_counter() - t < seconds:
         pass
@@ -575,7 +580,6 @@ def time_region(world, dist, torch, body, dev, streams=()):
     """barrier + synchronize, body(), settle + synchronize + barrier; max over ranks."""
     if world > 1:
         dist.barrier()
-    host_warm()
     GPU.sync()
     t0 = time.perf_counter()
     body()
@@ -683,11 +687,11 @@ def run_c4(args, world, rank, local, dev, frames):
                         w.wait()
                 pend[k] = None
 
+    host_warm()
     for i in range(args.warmup):
         step(i)
     drain()
     GPU.settle(streams)
-    GPU.sync()
 
     def body():
         for i in range(args.steps):

@@ -86,8 +86,18 @@ def region(v, i0):
         while not all(ev.query() for ev in evs0):
             pass
         torch.cuda.synchronize()
+    if "prespin" in mods:  # the host spin before the warmup steps (the GPU busy until the region)
+        t = time.perf_counter()
+        while time.perf_counter() - t < 3e-3:
+            pass
     # warmup steps (untimed), as the bench
     run_base(i0, a.warmup, ns)
+    if "settlewarm" in mods:  # wait for the warmup by polling events (the host thread never sleeps)
+        evw = [torch.cuda.Event() for _ in range(ns)]
+        for q in range(ns):
+            evw[q].record(streams[q])
+        while not all(ev.query() for ev in evw):
+            pass
     torch.cuda.synchronize()
     pre = [fast_args(i, ns) for i in range(i0 + a.warmup, i0 + a.warmup + K)] if name != "base" else None
     spin = name == "fast_spin" or "settle" in mods
