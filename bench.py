@@ -25,6 +25,7 @@ Prints ONE JSON line on rank 0 (see the contract in DESIGN.md §5).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import platform
@@ -429,6 +430,7 @@ def main():
         dist.barrier()
     # the host spin first, then the warmup steps right before the region: the GPU stays busy up
     # to it (an idle GPU before a 20-step region cost ~9 us, tools/region_ab.py, round 3)
+    gc.collect()
     host_warm()
     for i in range(args.warmup):
         step(i, i, args.warmup)
@@ -438,10 +440,12 @@ def main():
         last.clear()  # the checks below cover the timed region's gathers
         issued.clear()
 
-    # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks
+    # ---- timed region: K steps, barrier + synchronize on both sides, max over ranks (Python's
+    # garbage collector off inside it, as timeit does: a collection is tens of us in a ~400-us region)
     if world > 1:
         dist.barrier()
     GPU.sync()
+    gc.disable()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, i, args.steps)
@@ -451,6 +455,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -581,6 +586,7 @@ def time_region(world, dist, torch, body, dev, streams=()):
     if world > 1:
         dist.barrier()
     GPU.sync()
+    gc.disable()
     t0 = time.perf_counter()
     body()
     GPU.settle(streams)
@@ -588,6 +594,7 @@ def time_region(world, dist, torch, body, dev, streams=()):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -687,6 +694,7 @@ def run_c4(args, world, rank, local, dev, frames):
                         w.wait()
                 pend[k] = None
 
+    gc.collect()
     host_warm()
     for i in range(args.warmup):
         step(i)
