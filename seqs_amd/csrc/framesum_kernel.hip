@@ -172,6 +172,16 @@ __device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const Lane
 }
 
 // Z operator from a plain [4][256] table (a few uses per frame).
+#ifdef FS_NOCONF
+// diagnostic build (results wrong): the combine's lookups at conflict-free entries (lane & 31),
+// still dependent on `a`
+__device__ __forceinline__ uint32_t zplain_nc(const char* lds, uint32_t a, uint32_t base) {
+    uint32_t z;
+    asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(a));
+    const uint32_t e = ((z | __lane_id()) & 31u) << 2;
+    return lds32(lds, base + e) ^ lds32(lds, base + 1024 + e) ^ lds32(lds, base + 2048 + e) ^ lds32(lds, base + 3072 + e);
+}
+#endif
 __device__ __forceinline__ uint32_t zplain(const char* lds, uint32_t a, uint32_t base) {
     return lds32(lds, base + ((a & 0xffu) << 2)) ^ lds32(lds, base + 1024 + (((a >> 8) & 0xffu) << 2)) ^
            lds32(lds, base + 2048 + (((a >> 16) & 0xffu) << 2)) ^ lds32(lds, base + 3072 + ((a >> 24) << 2));
@@ -1107,12 +1117,21 @@ struct LayA1 : LayoutA {
     static constexpr uint32_t kCapStride = 3072;
     static constexpr int kCapBlocks = 3;
     // the combine's shifts Z_(4c), c = 1..3, and Z_(16a), a = 1..3
+#ifdef FS_NOCONF
+    __device__ static __forceinline__ uint32_t z4c(const char* lds, uint32_t v, uint32_t c) {
+        return zplain_nc(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
+    }
+    __device__ static __forceinline__ uint32_t z16a(const char* lds, uint32_t v, uint32_t a) {
+        return zplain_nc(lds, v, a == 1u ? kLdsZ16 : a == 2u ? kLdsZ32 : kLdsZ48);
+    }
+#else
     __device__ static __forceinline__ uint32_t z4c(const char* lds, uint32_t v, uint32_t c) {
         return zplain(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
     }
     __device__ static __forceinline__ uint32_t z16a(const char* lds, uint32_t v, uint32_t a) {
         return zplain(lds, v, a == 1u ? kLdsZ16 : a == 2u ? kLdsZ32 : kLdsZ48);
     }
+#endif
 };
 
 // `report` = the host-mapped report word's address in bits 0..47, the launch id in bits 48..63
@@ -1334,8 +1353,26 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             const uint32_t v2 = Lay::z16a(lds, v, a4);
             Y ^= a4 ? v2 : v;
         }
+#ifdef FS_XR_LANE
+        {  // diagnostic build: FS_XR_LANE extra dependent table rounds on every lane (results unchanged)
+            uint32_t z = Y, zero;
+#pragma unroll
+            for (int i = 0; i < FS_XR_LANE; ++i) z = zplain(lds, z, kLdsZ16);
+            asm volatile("v_mov_b32 %0, 0" : "=v"(zero) : "v"(z));
+            Y ^= zero;
+        }
+#endif
         Y ^= dpp_quad<kQuadXor1>(Y);
         Y ^= dpp_quad<kQuadXor2>(Y);
+#ifdef FS_XR_FIN
+        if (parser) {  // diagnostic build: FS_XR_FIN extra dependent table rounds on the parser lanes
+            uint32_t z = Y, zero;
+#pragma unroll
+            for (int i = 0; i < FS_XR_FIN; ++i) z = zplain(lds, z, kLdsZ16);
+            asm volatile("v_mov_b32 %0, 0" : "=v"(zero) : "v"(z));
+            Y ^= zero;
+        }
+#endif
         // checksum over the 4 lanes of the group, each lane first folded mod 65535 (the finish
         // only needs the total mod 65535; the fold keeps every partial < 2^18)
         cs = (cs & 0xffffu) + (cs >> 16);

@@ -190,14 +190,23 @@ def crc32_model_al(buf: bytes, S: int, length: int, base_phase: int = 0) -> int:
                     d &= tail_mask
                 if x < nd:
                     A[lane][j] = apply(Z64, A[lane][j]) ^ d ^ c
+    # combine: stream j of a lane needs Z_4s, s = (K - j) mod 16, K = q - 4 lane = 4 a + C. Streams
+    # j <= C have (a, s & 3) = (a, C - j), the others ((a - 1) & 3, 4 + C - j). Sorted by s & 3
+    # (B_c = A_((C - c) & 3)), one round of Z4/Z8/Z12 and one of Z_16a per class.
     q = 15 - e
     Y = 0
     for lane in range(4):
-        for j in range(4):
-            s = (q - 4 * lane - j) & 15
-            v = A[lane][j]
-            if s:
-                v = apply(op_table(4 * s), v)
-            Y ^= v
+        K = (q - 4 * lane) & 15
+        a, C = K >> 2, K & 3
+        B = [A[lane][(C - c) & 3] for c in range(4)]
+        T = [B[0]] + [apply(op_table(4 * c), B[c]) for c in (1, 2, 3)]
+        V1 = V2 = 0
+        for c in range(4):
+            if c <= C:
+                V1 ^= T[c]
+            else:
+                V2 ^= T[c]
+        a2 = (a - 1) & 3
+        Y ^= (apply(op_table(16 * a), V1) if a else V1) ^ (apply(op_table(16 * a2), V2) if a2 else V2)
     t = (4 - (E & 3)) & 3
     return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
