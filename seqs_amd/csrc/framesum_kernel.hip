@@ -172,16 +172,6 @@ __device__ __forceinline__ uint32_t zrep(const char* lds, uint32_t a, const Lane
 }
 
 // Z operator from a plain [4][256] table (a few uses per frame).
-#ifdef FS_NOCONF
-// diagnostic build (results wrong): the combine's lookups at conflict-free entries (lane & 31),
-// still dependent on `a`
-__device__ __forceinline__ uint32_t zplain_nc(const char* lds, uint32_t a, uint32_t base) {
-    uint32_t z;
-    asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(a));
-    const uint32_t e = ((z | __lane_id()) & 31u) << 2;
-    return lds32(lds, base + e) ^ lds32(lds, base + 1024 + e) ^ lds32(lds, base + 2048 + e) ^ lds32(lds, base + 3072 + e);
-}
-#endif
 __device__ __forceinline__ uint32_t zplain(const char* lds, uint32_t a, uint32_t base) {
     return lds32(lds, base + ((a & 0xffu) << 2)) ^ lds32(lds, base + 1024 + (((a >> 8) & 0xffu) << 2)) ^
            lds32(lds, base + 2048 + (((a >> 16) & 0xffu) << 2)) ^ lds32(lds, base + 3072 + ((a >> 24) << 2));
@@ -1116,22 +1106,11 @@ struct LayA1 : LayoutA {
     static constexpr uint32_t kHdr = kLdsHdr;
     static constexpr uint32_t kCapStride = 3072;
     static constexpr int kCapBlocks = 3;
-    // the combine's shifts Z_(4c), c = 1..3, and Z_(16a), a = 1..3
-#ifdef FS_NOCONF
-    __device__ static __forceinline__ uint32_t z4c(const char* lds, uint32_t v, uint32_t c) {
-        return zplain_nc(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
-    }
+    // Z_(16a)(v), a = 0..3 (the lookups run for a = 0 too; the select drops them)
     __device__ static __forceinline__ uint32_t z16a(const char* lds, uint32_t v, uint32_t a) {
-        return zplain_nc(lds, v, a == 1u ? kLdsZ16 : a == 2u ? kLdsZ32 : kLdsZ48);
+        const uint32_t y = zplain(lds, v, a == 1u ? kLdsZ16 : a == 2u ? kLdsZ32 : kLdsZ48);
+        return a ? y : v;
     }
-#else
-    __device__ static __forceinline__ uint32_t z4c(const char* lds, uint32_t v, uint32_t c) {
-        return zplain(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
-    }
-    __device__ static __forceinline__ uint32_t z16a(const char* lds, uint32_t v, uint32_t a) {
-        return zplain(lds, v, a == 1u ? kLdsZ16 : a == 2u ? kLdsZ32 : kLdsZ48);
-    }
-#endif
 };
 
 // `report` = the host-mapped report word's address in bits 0..47, the launch id in bits 48..63
@@ -1338,41 +1317,31 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
 
         // ---- combine the 16 streams of each frame. Stream j of lane gl (row position 4 gl + j)
         // is shifted by its distance in dwords to the frame's last dword, at position
-        // q = 15 - ealign() of the last row: (q - 4 gl - j) mod 16 (the streams past q skipped the
-        // last row), as Z_(16 a) Z_(4 c) with s = 4 a + c; then xor over the group's 4 lanes.
+        // q = 15 - ealign() of the last row: s = (K - j) mod 16 with K = (q - 4 gl) mod 16 = 4 a + C
+        // (the streams past q skipped the last row); then xor over the group's 4 lanes.
+        // Streams j <= C need Z_(16 a) Z_(4 (C - j)), the others Z_(16 ((a - 1) & 3)) Z_(4 (4 + C - j)).
+        // Sorted by their Z4 class c (B_c = A_((C - c) & 3): the registers reversed, then rotated
+        // by C), that is one round of Z4 / Z8 / Z12 with a fixed table per register and one round
+        // of Z_(16 a) per class: 5 lookups in 2 dependent rounds (tests/kernel_model.py).
         // The parked parse, read by every lane now: its LDS round trip overlaps the combine's.
         const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
-        const uint32_t kq = (uint32_t)(15 - T.ealign() - 4 * (int)gl);
-        uint32_t Y = 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t sh = (kq - j) & 15u, c = sh & 3u, a4 = sh >> 2;
-            uint32_t v = A[j];
-            const uint32_t v1 = Lay::z4c(lds, v, c);
-            v = c ? v1 : v;
-            const uint32_t v2 = Lay::z16a(lds, v, a4);
-            Y ^= a4 ? v2 : v;
+        const uint32_t K = (uint32_t)(15 - T.ealign() - 4 * (int)gl) & 15u;
+        const uint32_t a = K >> 2, C = K & 3u;
+        uint32_t Y;
+        {
+            const bool r1 = (C & 1u) != 0u, r2 = (C & 2u) != 0u;
+            // reversed: (A0, A3, A2, A1); rotated by 1 then by 2 where C has those bits
+            const uint32_t x0 = r1 ? A[1] : A[0], x1 = r1 ? A[0] : A[3], x2 = r1 ? A[3] : A[2], x3 = r1 ? A[2] : A[1];
+            const uint32_t b0 = r2 ? x2 : x0, b1 = r2 ? x3 : x1, b2 = r2 ? x0 : x2, b3 = r2 ? x1 : x3;
+            const uint32_t t1 = zplain(lds, b1, kLdsZfin);  // Z4
+            const uint32_t t2 = zplain(lds, b2, kLdsZ8);
+            const uint32_t t3 = zplain(lds, b3, kLdsZ12);
+            const uint32_t v1 = b0 ^ (C >= 1u ? t1 : 0u) ^ (C >= 2u ? t2 : 0u) ^ (C == 3u ? t3 : 0u);
+            const uint32_t v2 = xor3(b0 ^ t1, t2, t3) ^ v1;
+            Y = Lay::z16a(lds, v1, a) ^ Lay::z16a(lds, v2, (a - 1u) & 3u);
         }
-#ifdef FS_XR_LANE
-        {  // diagnostic build: FS_XR_LANE extra dependent table rounds on every lane (results unchanged)
-            uint32_t z = Y, zero;
-#pragma unroll
-            for (int i = 0; i < FS_XR_LANE; ++i) z = zplain(lds, z, kLdsZ16);
-            asm volatile("v_mov_b32 %0, 0" : "=v"(zero) : "v"(z));
-            Y ^= zero;
-        }
-#endif
         Y ^= dpp_quad<kQuadXor1>(Y);
         Y ^= dpp_quad<kQuadXor2>(Y);
-#ifdef FS_XR_FIN
-        if (parser) {  // diagnostic build: FS_XR_FIN extra dependent table rounds on the parser lanes
-            uint32_t z = Y, zero;
-#pragma unroll
-            for (int i = 0; i < FS_XR_FIN; ++i) z = zplain(lds, z, kLdsZ16);
-            asm volatile("v_mov_b32 %0, 0" : "=v"(zero) : "v"(z));
-            Y ^= zero;
-        }
-#endif
         // checksum over the 4 lanes of the group, each lane first folded mod 65535 (the finish
         // only needs the total mod 65535; the fold keeps every partial < 2^18)
         cs = (cs & 0xffffu) + (cs >> 16);
