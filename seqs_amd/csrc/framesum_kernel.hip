@@ -1267,7 +1267,19 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 else lean_row<Lay::kRegion>(lds, keys, pf[i], A, cs);
                 if (r0 == 0 && T.cap) {  // the frame's first blocks into the header slot
                     const uint32_t k = (uint32_t)(i - T.r0f);
-                    if (k < (uint32_t)Lay::kCapBlocks) *reinterpret_cast<u32x4*>(lds + hw + (4u * k + gl) * 256u + grp * 16u) = pf[i];
+                    if (k < (uint32_t)Lay::kCapBlocks) {
+                        // two 8-B stores, the odd group lanes writing their upper half first: a
+                        // group's 4 lanes write the same 16-B column of 4 cells 256 B apart, so one
+                        // 16-B store each hits one bank quad 4 times; this way 2 lanes share banks
+                        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                        const u32x4 v = pf[i];
+                        const bool s1 = (gl & 1u) != 0u;
+                        const u32x2 h0 = s1 ? u32x2{v.z, v.w} : u32x2{v.x, v.y};
+                        const u32x2 h1 = s1 ? u32x2{v.x, v.y} : u32x2{v.z, v.w};
+                        const uint32_t cb = hw + (4u * k + gl) * 256u + grp * 16u + ((gl & 1u) << 3);
+                        *reinterpret_cast<u32x2*>(lds + cb) = h0;
+                        *reinterpret_cast<u32x2*>(lds + (cb ^ 8u)) = h1;
+                    }
                 }
                 if (kRefill) {
                     const int rn = rel + kRowDwords * kPfA;
