@@ -276,7 +276,8 @@ func (m *GPUs) DigestBatch(frames [][]byte, mtu uint16, out []Digest, verdicts [
 // the HBM of several GPUs (GPUDirect RDMA) are digested where they lie, round-robin sharded
 // (global frame i is frame i / N of shard i % N; eth/crc.go:12-17: CRC791 is per call, so frames
 // are independent); only the 8-byte digests and 1-byte verdicts travel, over xGMI, to the first
-// device (ncclGather), where a de-interleave kernel restores global order. The consumer is the
+// device (chunk by chunk, grouped ncclSend/ncclRecv), where a de-interleave kernel restores global
+// order. The consumer is the
 // same as DigestBatch's: stacks.PortStack.RecvEth (stacks/portstack.go:163) -> :240 / :303.
 type Group struct {
 	g    *C.fs_group

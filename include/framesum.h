@@ -196,11 +196,16 @@ uint64_t fs_shard_count(uint64_t n, uint32_t nshards, uint32_t shard);
 
 /* Digest a global batch sharded round-robin over the group's devices. frames[k], offsets[k],
  * lengths[k] are DEVICE pointers on the group's k-th device describing shard k (its
- * fs_shard_count(n, ndev, k) frames, laid out as fs_digest_batch expects). Every shard's
- * kernel runs on its own device at once; the digests and verdicts are then gathered to the
- * first device with ncclGather and put back in global frame order there by a de-interleave
- * kernel: out (n digests) and status (n bytes, nullable) are DEVICE pointers on the group's
- * first device. Returns when they are written. At most 2^31 frames per shard. */
+ * fs_shard_count(n, ndev, k) frames, laid out as fs_digest_batch expects). The call works in
+ * chunks of the shards' rows (at most 8, ~32K rows each). For each chunk, every device digests
+ * its rows on its own compute stream; its digest and verdict pieces then go to the first
+ * device by grouped point-to-point RCCL transfers (ncclSend / ncclRecv on a second stream per
+ * device), and a de-interleave kernel there puts that chunk's frames in global order. So a
+ * chunk's transfer and de-interleave overlap the next chunk's kernels. out (n digests) and
+ * status (n bytes, nullable) are DEVICE pointers on the group's first device. Returns when
+ * they are written; on an error return every stream of the group has been drained first, so
+ * no work of the failed call is still in flight. At most 2^31 frames per shard. N > 1
+ * devices has not run on hardware (the build boxes have one GPU). */
 fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, const uint64_t* const* offsets,
                                   const uint32_t* const* lengths, uint64_t n, uint32_t mtu, fs_digest* out,
                                   uint8_t* status);

@@ -47,8 +47,9 @@ struct fs_ctx {
     int device = 0;
     int num_cus = 0;
     FsTables* d_tables = nullptr;
-    // fault injection for the host-staged pipeline's tests (FS_FAULT_CHUNK=k: fs_digest_batch_host
-    // fails with FS_E_NOMEM at chunk k, after the earlier chunks' work and chunk k's copy are queued)
+    // fault injection for the host-staged pipeline's tests, settable only through the test
+    // library's fs_test_set_fault (-DFS_TEST_HOOKS): fs_digest_batch_host fails with FS_E_NOMEM at
+    // chunk k, after the earlier chunks' work and chunk k's copy are queued. -1 in the product.
     long fault_chunk = -1;
     // host-mapped word the kernels set when a batch has widely mixed lengths (launch_digest)
     volatile uint32_t* h_report = nullptr;
@@ -198,10 +199,6 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
     framesum::build_tables(h);
     e = hipMalloc(&ctx->d_tables, sizeof(FsTables));
     if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, h, sizeof(FsTables), hipMemcpyHostToDevice);
-    if (e == hipSuccess) {
-        const char* fc = std::getenv("FS_FAULT_CHUNK");
-        if (fc && *fc) ctx->fault_chunk = std::atol(fc);
-    }
     if (e == hipSuccess) {
         void* hp = nullptr;
         e = hipHostMalloc(&hp, 64, hipHostMallocMapped);
@@ -379,7 +376,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
             if (st != FS_SUCCESS) return st;
         }
         if ((long)chunk == ctx->fault_chunk)
-            return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: injected failure (FS_FAULT_CHUNK)");
+            return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: injected failure (test hook)");
         FS_HIP(ctx, hipStreamWaitEvent(ks, sl.copied, 0));
         // the kernel addresses frame i at base + offsets[i]: base = staging - cpy_lo (4-B aligned)
         const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
@@ -579,6 +576,15 @@ int fs_ctx_last_kernel(const fs_ctx* ctx) {
     if (!ctx || !ctx->h_report) return FS_E_INVALID;
     return (int)ctx->h_report[framesum::kReportChosen];
 }
+
+#ifdef FS_TEST_HOOKS
+// Test library only (-DFS_TEST_HOOKS): fs_digest_batch_host on ctx fails at chunk `chunk` (-1: never).
+fs_status fs_test_set_fault(fs_ctx* ctx, long chunk) {
+    if (!ctx) return FS_E_INVALID;
+    ctx->fault_chunk = chunk;
+    return FS_SUCCESS;
+}
+#endif
 
 fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out) {
     if (!ctx || !out) return FS_E_INVALID;

@@ -1,11 +1,12 @@
 // framesum multi-GPU group (include/framesum.h: fs_group_*, fs_digest_batch_sharded): one host
 // process drives every GPU of a node. Each device digests its round-robin shard with the
-// gfx950 kernel (through fs_digest_batch on its own context and stream); RCCL (ncclGather over
-// xGMI) brings the 8-byte digests and 1-byte verdicts to the first device, where the
-// de-interleave kernel (framesum_shard.hip) restores global frame order. Frames are
-// independent (eth/crc.go:12-17), so the gather is the only collective. The batch goes in
-// chunks (framesum_plan.h chunk_rows): chunk c's transfer and de-interleave run on a second
-// stream per device while the devices digest chunk c+1.
+// gfx950 kernel (through fs_digest_batch on its own context and stream); grouped point-to-point
+// RCCL transfers (ncclSend / ncclRecv over xGMI) bring the 8-byte digests and 1-byte verdicts to
+// the first device, where the de-interleave kernel (framesum_shard.hip) restores global frame
+// order. Frames are independent (eth/crc.go:12-17), so this transfer is the only exchange. The
+// batch goes in chunks (framesum_plan.h chunk_plan): chunk c's transfer and de-interleave run on
+// a second stream per device while the devices digest chunk c+1. N > 1 devices is unverified on
+// hardware (one GPU per build box); tests/csrc/test_plan.cpp replays the chunk plan on the host.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -28,6 +29,7 @@ struct fs_group {
     std::vector<uint8_t*> send;  // per device k >= 1: its slab; device 0 sends in place from recv
     uint8_t* recv = nullptr;     // first device: n slabs back to back
     uint64_t cap_slab = 0;       // bytes per slab currently allocated
+    long fault_chunk = -1;       // test library only (fs_test_group_set_fault): fail at this chunk
     std::string err;
 };
 
@@ -78,6 +80,23 @@ fs_status ensure_slabs(fs_group* g, uint64_t sb) {
             return gset(g, FS_E_NOMEM, "fs_digest_batch_sharded: hipMalloc of a shard slab failed");
     g->cap_slab = sb;
     return FS_SUCCESS;
+}
+
+// Best-effort drain of every stream of the group (compute and transfer), so that an error exit
+// leaves no kernel, transfer or de-interleave of the failed call in flight: the next call's
+// kernels then never overwrite a slab an earlier ncclSend still reads, and nothing writes the
+// caller's out/status after the error return.
+void quiesce_group(fs_group* g) {
+    for (int k = 0; k < g->n; ++k) {
+        (void)hipSetDevice(g->dev[k]);
+        if (g->stream[k]) (void)hipStreamSynchronize(g->stream[k]);
+        if (g->xfer[k]) (void)hipStreamSynchronize(g->xfer[k]);
+    }
+}
+
+fs_status fail_group(fs_group* g, fs_status code, const std::string& msg) {
+    quiesce_group(g);
+    return gset(g, code, msg);
 }
 
 }  // namespace
@@ -166,6 +185,19 @@ fs_status fs_group_destroy(fs_group* g) {
 
 const char* fs_group_last_error(const fs_group* g) { return g ? g->err.c_str() : g_group_create_err.c_str(); }
 
+#ifdef FS_TEST_HOOKS
+// Test library only (seqs_amd/lib/test/libframesum_test.so, -DFS_TEST_HOOKS): the next
+// fs_digest_batch_sharded calls on g fail at chunk `chunk` (-1: never), after the earlier chunks'
+// kernels, transfers and de-interleaves are queued.
+fs_status fs_test_group_set_fault(fs_group* g, long chunk) {
+    if (!g) return FS_E_INVALID;
+    g->fault_chunk = chunk;
+    return FS_SUCCESS;
+}
+#endif
+
+
+
 fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, const uint64_t* const* offsets,
                                   const uint32_t* const* lengths, uint64_t n, uint32_t mtu, fs_digest* out,
                                   uint8_t* status) {
@@ -182,22 +214,28 @@ fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, con
     for (uint32_t k = 0; k < N; ++k)
         if (framesum::plan::shard_count(n, N, k) > 0 && (!frames[k] || !offsets[k] || !lengths[k]))
             return gset(g, FS_E_INVALID, "fs_digest_batch_sharded: null shard pointer");
-    const uint64_t want = (m + kChunkRows - 1) / kChunkRows;
-    const uint64_t R = framesum::plan::chunk_rows(m, (uint32_t)(want < kMaxChunks ? want : kMaxChunks));
-    const uint32_t C = framesum::plan::chunk_count(m, R);
+    std::vector<framesum::plan::ChunkXfer> plan;
+    try {
+        framesum::plan::chunk_plan(n, N, kMaxChunks, kChunkRows, plan);
+    } catch (const std::bad_alloc&) {
+        return gset(g, FS_E_NOMEM, "fs_digest_batch_sharded: out of host memory");
+    }
     hipError_t e = hipSuccess;
-    for (uint32_t c = 0; c < C; ++c) {
-        const uint64_t lo = (uint64_t)c * R, hi = lo + R < m ? lo + R : m;
+    for (uint32_t c = 0; c < (uint32_t)plan.size(); ++c) {
+        const framesum::plan::ChunkXfer& x = plan[c];
+        if ((long)c == g->fault_chunk)  // test library only: earlier chunks are in flight here
+            return fail_group(g, FS_E_HIP, "fs_digest_batch_sharded: injected fault at chunk " + std::to_string(c));
         // chunk c of every shard on its own device's compute stream, into its slab (the first
         // device: in place in the gather buffer)
         for (uint32_t k = 0; k < N; ++k) {
-            const uint64_t r = framesum::plan::shard_rows_in(n, N, k, lo, hi);
+            const uint64_t r = framesum::plan::shard_rows_in(n, N, k, x.lo, x.hi);
             if (r == 0) continue;
-            st = fs_digest_batch(g->ctx[k], frames[k], offsets[k] + lo, lengths[k] + lo, (uint32_t)r, mtu,
-                                 reinterpret_cast<fs_digest*>(g->send[k] + 8 * lo), g->send[k] + 8 * m + lo,
+            st = fs_digest_batch(g->ctx[k], frames[k], offsets[k] + x.lo, lengths[k] + x.lo, (uint32_t)r, mtu,
+                                 reinterpret_cast<fs_digest*>(g->send[k] + 8 * x.lo), g->send[k] + 8 * m + x.lo,
                                  g->stream[k]);
             if (st != FS_SUCCESS)
-                return gset(g, st, "fs_digest_batch_sharded: shard " + std::to_string(k) + ": " + fs_last_error(g->ctx[k]));
+                return fail_group(g, st, "fs_digest_batch_sharded: shard " + std::to_string(k) + ": " +
+                                             fs_last_error(g->ctx[k]));
         }
         // its transfer waits for those kernels only: the compute streams go on with chunk c+1
         for (uint32_t k = 0; k < N && e == hipSuccess; ++k) {
@@ -210,30 +248,31 @@ fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, con
         // the chunk's digest and verdict pieces of every other shard to the first device, into
         // their places in the slabs (point-to-point pairs in one group: the gather of this chunk)
         ncclResult_t r = ncclGroupStart();
-        for (uint32_t k = 1; k < N && r == ncclSuccess; ++k) {
-            const uint64_t rk = framesum::plan::shard_rows_in(n, N, k, lo, hi);
-            if (rk == 0) continue;
-            uint8_t* at = g->recv + (uint64_t)k * sb;
-            r = ncclSend(g->send[k] + 8 * lo, 8 * rk, ncclUint8, 0, g->comm[k], g->xfer[k]);
-            if (r == ncclSuccess) r = ncclSend(g->send[k] + 8 * m + lo, rk, ncclUint8, 0, g->comm[k], g->xfer[k]);
-            if (r == ncclSuccess) r = ncclRecv(at + 8 * lo, 8 * rk, ncclUint8, (int)k, g->comm[0], g->xfer[0]);
-            if (r == ncclSuccess) r = ncclRecv(at + 8 * m + lo, rk, ncclUint8, (int)k, g->comm[0], g->xfer[0]);
+        for (const framesum::plan::Piece& p : x.pieces) {
+            if (r != ncclSuccess) break;
+            const uint32_t k = p.shard;
+            r = ncclSend(g->send[k] + p.send_dig, 8 * p.rows, ncclUint8, 0, g->comm[k], g->xfer[k]);
+            if (r == ncclSuccess) r = ncclSend(g->send[k] + p.send_st, p.rows, ncclUint8, 0, g->comm[k], g->xfer[k]);
+            if (r == ncclSuccess) r = ncclRecv(g->recv + p.recv_dig, 8 * p.rows, ncclUint8, (int)k, g->comm[0], g->xfer[0]);
+            if (r == ncclSuccess) r = ncclRecv(g->recv + p.recv_st, p.rows, ncclUint8, (int)k, g->comm[0], g->xfer[0]);
         }
         const ncclResult_t r2 = ncclGroupEnd();
         if (r != ncclSuccess || r2 != ncclSuccess)
-            return gset(g, FS_E_HIP, std::string("fs_digest_batch_sharded: chunk gather: ") +
-                                         ncclGetErrorString(r != ncclSuccess ? r : r2));
+            return fail_group(g, FS_E_HIP, std::string("fs_digest_batch_sharded: chunk gather: ") +
+                                               ncclGetErrorString(r != ncclSuccess ? r : r2));
         e = hipSetDevice(g->dev[0]);
-        if (e == hipSuccess)
-            e = framesum::launch_deinterleave(g->recv, N, n, out, status, g->xfer[0], lo * N, hi * N);
+        if (e == hipSuccess) e = framesum::launch_deinterleave(g->recv, N, n, out, status, g->xfer[0], x.g0, x.g1);
         if (e != hipSuccess) break;
     }
+    if (e != hipSuccess)
+        return fail_group(g, FS_E_HIP, std::string("fs_digest_batch_sharded: ") + hipGetErrorString(e));
     for (uint32_t k = 0; k < N && e == hipSuccess; ++k) {
         e = hipSetDevice(g->dev[k]);
         if (e == hipSuccess) e = hipStreamSynchronize(g->stream[k]);
         if (e == hipSuccess) e = hipStreamSynchronize(g->xfer[k]);
     }
-    if (e != hipSuccess) return gset(g, FS_E_HIP, std::string("fs_digest_batch_sharded: ") + hipGetErrorString(e));
+    if (e != hipSuccess)
+        return fail_group(g, FS_E_HIP, std::string("fs_digest_batch_sharded: ") + hipGetErrorString(e));
     return FS_SUCCESS;
 }
 

@@ -72,9 +72,9 @@ constexpr int kPrioMinRows = 36;  // the one-pass kernel's progress-based priori
 constexpr int kHdrDwords = 32;
 constexpr uint32_t kHdrWaveBytes = 4u * kHdrDwords * kFramesPerTile;  // 2 KB
 
-// LDS map (bytes). [0, 104 KB) holds the tables: the plain tables first (copied by LDS-DMA
-// from FsTables, where they follow region A), then region A (built in place from the Z64
-// basis). Every table address is a constant below 64 KB plus a lane-dependent part, so
+// LDS map (bytes). [0, 104 KB) holds the tables: the plain tables first, then region A, both
+// built in place by VALU from their GF(2) bases (build_region_a; FsTables keeps the full image
+// only as the layout's reference). Every table address is a constant below 64 KB plus a lane-dependent part, so
 // hipcc folds the constant into the ds_read offset field instead of holding it in a VGPR.
 constexpr uint32_t kLdsZ32 = 0;
 constexpr uint32_t kLdsZ16 = kLdsZ32 + 4096;

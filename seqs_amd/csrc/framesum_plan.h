@@ -48,6 +48,44 @@ constexpr uint64_t shard_rows_in(uint64_t n, uint32_t nshards, uint32_t shard, u
     return (hi < c ? hi : c) > lo ? (hi < c ? hi : c) - lo : 0;
 }
 
+// The transfers of one chunk of fs_digest_batch_sharded: for every shard k >= 1 with rows in
+// the chunk, its digest piece and its verdict piece go from its own slab (send offsets) to
+// slab k of the first device's gather buffer (recv offsets); shard 0's kernel writes in place
+// there. The first device then de-interleaves the global frames [g0, g1).
+struct Piece {
+    uint32_t shard;           // k >= 1
+    uint64_t rows;            // rk = shard_rows_in(n, N, k, lo, hi) > 0
+    uint64_t send_dig, send_st;  // byte offsets in shard k's slab: 8 lo, 8 m + lo
+    uint64_t recv_dig, recv_st;  // byte offsets in the gather buffer: k sb + 8 lo, k sb + 8 m + lo
+};
+struct ChunkXfer {
+    uint64_t lo, hi;   // local rows [lo, hi) of every shard
+    uint64_t g0, g1;   // global frames [g0, g1) = [lo N, min(hi N, n))
+    std::vector<Piece> pieces;
+};
+// The chunk plan of a sharded call: nchunks_max chunks at most, about target_rows rows each.
+inline void chunk_plan(uint64_t n, uint32_t N, uint32_t nchunks_max, uint64_t target_rows, std::vector<ChunkXfer>& out) {
+    out.clear();
+    if (N == 0 || n == 0) return;
+    const uint64_t m = shard_rows(n, N), sb = slab_bytes(m);
+    const uint64_t want = target_rows ? (m + target_rows - 1) / target_rows : 1;
+    const uint64_t R = chunk_rows(m, (uint32_t)(want < nchunks_max ? want : nchunks_max));
+    const uint32_t C = chunk_count(m, R);
+    for (uint32_t c = 0; c < C; ++c) {
+        ChunkXfer x;
+        x.lo = (uint64_t)c * R;
+        x.hi = x.lo + R < m ? x.lo + R : m;
+        x.g0 = x.lo * N;
+        x.g1 = x.hi * N < n ? x.hi * N : n;
+        for (uint32_t k = 1; k < N; ++k) {
+            const uint64_t rk = shard_rows_in(n, N, k, x.lo, x.hi);
+            if (rk == 0) continue;
+            x.pieces.push_back(Piece{k, rk, 8 * x.lo, 8 * m + x.lo, k * sb + 8 * x.lo, k * sb + 8 * m + x.lo});
+        }
+        out.push_back(x);
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Host-staged chunks.
 

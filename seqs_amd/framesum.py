@@ -87,20 +87,30 @@ class FramesumError(RuntimeError):
 
 
 _lib = None
+_libs: dict = {}
+
+# The test library: the same sources built with -DFS_TEST_HOOKS (seqs_amd/csrc/Makefile), which adds
+# the fault-injection setters fs_test_set_fault / fs_test_group_set_fault. Only tests load it; the
+# product library has no such hook (and reads no environment variable for one).
+TEST_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "test", "libframesum_test.so")
 
 
 def lib_path() -> str:
     return _LIB_PATH
 
 
-def load_library() -> ctypes.CDLL:
-    """Load libframesum.so (raises if it was not built: no fallback path exists)."""
+def load_library(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load libframesum.so (raises if it was not built: no fallback path exists). `path`: another
+    build of the same ABI (the test library, TEST_LIB_PATH)."""
     global _lib
-    if _lib is not None:
+    if path is None and _lib is not None:
         return _lib
-    if not os.path.exists(_LIB_PATH):
-        raise FramesumError(f"{_LIB_PATH} is missing — run __graft_entry__.build() (or make -C seqs_amd/csrc)")
-    lib = ctypes.CDLL(_LIB_PATH)
+    p = path or _LIB_PATH
+    if p in _libs:
+        return _libs[p]
+    if not os.path.exists(p):
+        raise FramesumError(f"{p} is missing — run __graft_entry__.build() (or make -C seqs_amd/csrc)")
+    lib = ctypes.CDLL(p)
     vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
     lib.fs_abi_version.restype = u32
     lib.fs_abi_version.argtypes = []
@@ -147,7 +157,14 @@ def load_library() -> ctypes.CDLL:
                                             vp, vp]
     lib.fs_deinterleave.restype = i32
     lib.fs_deinterleave.argtypes = [vp, vp, u32, u64, vp, vp, vp]
-    _lib = lib
+    if hasattr(lib, "fs_test_set_fault"):  # test library only
+        lib.fs_test_set_fault.restype = i32
+        lib.fs_test_set_fault.argtypes = [vp, ctypes.c_long]
+        lib.fs_test_group_set_fault.restype = i32
+        lib.fs_test_group_set_fault.argtypes = [vp, ctypes.c_long]
+    _libs[p] = lib
+    if path is None:
+        _lib = lib
     return lib
 
 
@@ -168,8 +185,8 @@ class Digest:
 class Engine:
     """One framesum context on one GPU (fs_ctx). Not thread-safe, like the C ctx."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load_library()
+    def __init__(self, device: int = 0, lib_path: Optional[str] = None):
+        self.lib = load_library(lib_path)
         self.device = device
         ctx = ctypes.c_void_p()
         st = self.lib.fs_ctx_create(device, ctypes.byref(ctx))
@@ -451,11 +468,11 @@ def shard_slab_bytes(n: int, nshards: int) -> int:
 class Group:
     """One host process driving several GPUs (fs_group): a context, a stream and an RCCL
     communicator per device. `digest_sharded` runs fs_digest_batch_sharded: every device digests
-    its round-robin shard, ncclGather brings the digests to the first device, a de-interleave
-    kernel restores global order there."""
+    its round-robin shard chunk by chunk, grouped ncclSend/ncclRecv bring each chunk's digests to
+    the first device, a de-interleave kernel restores global order there."""
 
-    def __init__(self, devices: Sequence[int]):
-        self.lib = load_library()
+    def __init__(self, devices: Sequence[int], lib_path: Optional[str] = None):
+        self.lib = load_library(lib_path)
         self.devices = [int(d) for d in devices]
         arr = (ctypes.c_int * len(self.devices))(*self.devices)
         g = ctypes.c_void_p()

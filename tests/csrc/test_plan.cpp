@@ -5,6 +5,7 @@
 // empty, zero-length, huge-offset, and with more contexts than frames.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -153,6 +154,81 @@ static void check_shards(uint64_t n, uint32_t N) {
     }
 }
 
+// The exact chunk loop of fs_digest_batch_sharded (framesum_group.cpp), replayed on the host with
+// memcpy standing in for ncclSend/ncclRecv: every shard's kernel writes its chunk rows into its
+// slab (shard 0 in place in the gather buffer), every Piece is copied, and each chunk's
+// de-interleave then reads only bytes that a kernel or a transfer of that chunk or an earlier one
+// has written, getting back global frame order. Ragged n, n < N and empty shards included.
+static void replay_chunks(uint64_t n, uint32_t N, uint32_t maxc, uint64_t target) {
+    std::vector<ChunkXfer> plan;
+    chunk_plan(n, N, maxc, target, plan);
+    if (n == 0) {
+        CHECK(plan.empty());
+        return;
+    }
+    const uint64_t m = shard_rows(n, N), sb = slab_bytes(m);
+    std::vector<std::vector<uint8_t>> send(N, std::vector<uint8_t>(sb, 0xCD));
+    std::vector<uint8_t> recv(N * sb, 0xAB), have(N * sb, 0);
+    std::vector<uint32_t> wrote(n, 0);
+    uint64_t g_next = 0;
+    for (const ChunkXfer& x : plan) {
+        CHECK(x.lo < x.hi && x.hi <= m && x.g0 == g_next && x.g0 == x.lo * N && x.g1 <= n && x.g0 < x.g1);
+        g_next = x.g1;
+        // the kernels: shard k writes local rows [lo, lo + rk)
+        for (uint32_t k = 0; k < N; ++k) {
+            const uint64_t rk = shard_rows_in(n, N, k, x.lo, x.hi);
+            uint8_t* slab = k == 0 ? recv.data() : send[k].data();
+            for (uint64_t j = x.lo; j < x.lo + rk; ++j) {
+                const uint64_t g = j * N + k;
+                CHECK(g < n);
+                std::memcpy(slab + 8 * j, &g, 8);
+                slab[8 * m + j] = (uint8_t)(g * 7 + 1);
+                if (k == 0) {
+                    std::fill(have.begin() + 8 * j, have.begin() + 8 * j + 8, 1);
+                    have[8 * m + j] = 1;
+                }
+            }
+        }
+        // the transfers
+        uint32_t prev = 0;
+        for (const Piece& p : x.pieces) {
+            const uint32_t k = p.shard;
+            CHECK(k >= 1 && k < N && k > prev);  // one piece per shard, in shard order
+            prev = k;
+            CHECK(p.rows == shard_rows_in(n, N, k, x.lo, x.hi) && p.rows > 0);
+            CHECK(p.send_dig == 8 * x.lo && p.send_st == 8 * m + x.lo);
+            CHECK(p.send_dig + 8 * p.rows <= 8 * m && p.send_st + p.rows <= sb);
+            CHECK(p.recv_dig == k * sb + p.send_dig && p.recv_st == k * sb + p.send_st);
+            CHECK(p.recv_dig + 8 * p.rows <= k * sb + 8 * m && p.recv_st + p.rows <= (k + 1) * sb);
+            std::memcpy(recv.data() + p.recv_dig, send[k].data() + p.send_dig, 8 * p.rows);
+            std::memcpy(recv.data() + p.recv_st, send[k].data() + p.send_st, p.rows);
+            std::fill(have.begin() + p.recv_dig, have.begin() + p.recv_dig + 8 * p.rows, 1);
+            std::fill(have.begin() + p.recv_st, have.begin() + p.recv_st + p.rows, 1);
+        }
+        for (uint32_t k = 1; k < N; ++k) {  // shards with rows in the chunk have a piece
+            bool listed = false;
+            for (const Piece& p : x.pieces) listed |= p.shard == k;
+            CHECK(listed == (shard_rows_in(n, N, k, x.lo, x.hi) > 0));
+        }
+        // the de-interleave of [g0, g1): only received bytes, global order back
+        for (uint64_t g = x.g0; g < x.g1; ++g) {
+            const uint64_t at = gathered_digest_at(g, N, m), sat = gathered_status_at(g, N, m);
+            bool ok = at + 8 <= recv.size() && sat < recv.size();
+            CHECK(ok);
+            if (!ok) continue;
+            for (int b = 0; b < 8; ++b) CHECK(have[at + b]);
+            CHECK(have[sat]);
+            uint64_t v = 0;
+            std::memcpy(&v, recv.data() + at, 8);
+            CHECK(v == g);
+            CHECK(recv[sat] == (uint8_t)(g * 7 + 1));
+            ++wrote[g];
+        }
+    }
+    CHECK(g_next == n);
+    for (uint64_t g = 0; g < n; ++g) CHECK(wrote[g] == 1);
+}
+
 int main() {
     std::mt19937_64 rng(12345);
     // chunks: every batch kind, several chunk sizes (small ones force many chunks)
@@ -183,6 +259,15 @@ int main() {
         for (uint64_t n : {uint64_t(0), uint64_t(1), uint64_t(2), uint64_t(7), uint64_t(8), uint64_t(9),
                            uint64_t(1000), uint64_t(65537), uint64_t(1) << 20})
             check_shards(n, N);
+    // the sharded call's chunk loop replayed with memcpy transfers, N = 1..8,
+    // ragged n, n < N, empty shards, the library's chunk parameters and small ones (many chunks)
+    for (uint32_t N = 1; N <= 8; ++N)
+        for (uint64_t n : {uint64_t(0), uint64_t(1), uint64_t(3), uint64_t(7), uint64_t(8), uint64_t(9), uint64_t(255),
+                           uint64_t(257), uint64_t(1000), uint64_t(4097), uint64_t(65537), uint64_t(300001)}) {
+            replay_chunks(n, N, 8, 32768);
+            replay_chunks(n, N, 8, 256);
+            replay_chunks(n, N, 3, 1);
+        }
     if (g_fail) {
         std::fprintf(stderr, "%d check(s) failed\n", g_fail);
         return 1;

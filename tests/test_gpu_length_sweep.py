@@ -65,6 +65,19 @@ def engine(request):
 
     e = Engine(0)
     e.set_kernel(request.param)
+    if request.param == 0:
+        # a context's first 16 launches run the mixed-length kernel whatever the
+        # batch, so without this the 'auto' column would re-test it. Uniform batches past that
+        # window move the automatic choice to the one-pass kernel, and the sweep's first launches
+        # then exercise the switch (its mixed-length report arrives launches late).
+        from seqs_amd import synth
+
+        ub, uo, ul = synth.uniform_batch(4096, 1500, seed=77)
+        ub, uo, ul = _dev(ub), _dev(uo), _dev(ul)
+        for _ in range(24):
+            e.digest_device(ub, uo, ul)
+        torch.cuda.synchronize()
+        assert e.last_kernel() == 4, "uniform traffic past the first 16 launches runs the one-pass kernel"
     yield e
     e.close()
 

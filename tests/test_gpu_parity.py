@@ -379,22 +379,24 @@ def test_set_kernel_accepts_shipped_variants_only():
         e.close()
 
 
-def test_host_fill_after_failed_digest(monkeypatch):
-    """a host-staged digest that fails half-way (FS_FAULT_CHUNK injects FS_E_NOMEM
-    at chunk 1, after chunk 0's kernel and chunk 1's copy are queued on the copy streams) must not
+def test_host_fill_after_failed_digest():
+    """a host-staged digest that fails half-way (the test library's
+    fs_test_set_fault injects FS_E_NOMEM at chunk 1, after chunk 0's kernel and chunk 1's copy are
+    queued on the copy streams; the product library has no such hook) must not
     leave copies in flight that corrupt the next host-staged call's staging: a TX fill right after
     it is byte-exact against the oracle, and so is a digest on a fresh context."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from seqs_amd import FramesumError
+    from seqs_amd.framesum import TEST_LIB_PATH
 
-    monkeypatch.setenv("FS_FAULT_CHUNK", "1")
-    e = Engine(0)
-    monkeypatch.delenv("FS_FAULT_CHUNK")
+    e = Engine(0, lib_path=TEST_LIB_PATH)
+    assert e.lib.fs_test_set_fault(e._ctx, 1) == 0
     try:
         big, boff, bln = synth.uniform_batch(30000, 1500, seed=31)  # 45 MB: three 16-MiB chunks
         with pytest.raises(FramesumError, match="injected"):
             e.digest_host(big, boff.astype(np.uint64), bln.astype(np.uint32))
+        assert e.lib.fs_test_set_fault(e._ctx, -1) == 0
         buf, off, ln = synth.mixed_batch(3000, seed=32)
         exp = buf.copy()
         edig, est = coracle.fill_batch(exp, off, ln, 0, 1)

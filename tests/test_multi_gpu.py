@@ -1,7 +1,7 @@
 """Multi-GPU paths on the real gfx950 engine, checked bit for bit against the CPU oracle.
 
 - C4 (BASELINE configs[3]): 1,048,576 x 1500-B frames sharded round-robin.
-  * fs_digest_batch_sharded (one process, RCCL ncclGather + de-interleave kernel) on the
+  * fs_digest_batch_sharded (one process, chunked RCCL ncclSend/ncclRecv + de-interleave kernel) on the
     box's devices (a 1-device communicator on a one-GPU box);
   * seqs_amd.shard.ShardedDigest with Engine.digest_device, world 2 and 4 over gloo, each
     rank a fresh child process on cuda:0.
@@ -85,6 +85,28 @@ def test_group_sharded_mixed_lengths():
         words, status = g.digest_sharded(shards_on(g.devices, buf, off, ln), len(ln), mtu=1514)
         dig, est = coracle.digest_batch(buf, off, ln, mtu=1514, nthreads=8)
         assert_equal_words(words.cpu().numpy(), status.cpu().numpy(), dig, est, "group mixed")
+    finally:
+        g.close()
+
+
+def test_group_fault_at_chunk1_then_exact(c4):
+    """an fs_digest_batch_sharded call that fails at chunk 1 (the test library's
+    fs_test_group_set_fault; chunk 0's kernels, transfers and de-interleave are queued by then)
+    drains every stream before returning, so the next call on the same group is bit-exact."""
+    from seqs_amd import FramesumError
+    from seqs_amd.framesum import TEST_LIB_PATH
+
+    buf, off, ln, dig, est = c4
+    devices = list(range(ndev()))
+    g = Group(devices, lib_path=TEST_LIB_PATH)
+    try:
+        shards = shards_on(devices, buf, off, ln)
+        assert g.lib.fs_test_group_set_fault(g._g, 1) == 0
+        with pytest.raises(FramesumError, match="injected fault at chunk 1"):
+            g.digest_sharded(shards, len(ln))
+        assert g.lib.fs_test_group_set_fault(g._g, -1) == 0
+        words, status = g.digest_sharded(shards, len(ln))
+        assert_equal_words(words.cpu().numpy(), status.cpu().numpy(), dig, est, "after injected fault")
     finally:
         g.close()
 
