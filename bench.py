@@ -127,7 +127,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=1000,
                    help="untimed launches first: throughput reaches its steady state only after several hundred "
                         "back-to-back launches (with 20 the timed steps measured 5-10%% lower)")
-    p.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2")
+    p.add_argument("--config", choices=["c2", "c3", "c4", "c5", "small"], default="c2",
+                   help="small: the reference's own benchmark shape (stacks/benchmark_test.go), 47-B UDP "
+                        "'hello' frames in 48-B slots")
     p.add_argument("--frames", type=int, default=None,
                    help="frames per GPU per step (c2/c3/c5; default 65,536, c5 16,384) or of the global batch (c4; "
                         "default 1,048,576)")
@@ -153,6 +155,12 @@ def parse():
                         "launches run first, over the streams, without the gather (reported as prewarm_launches)")
     p.add_argument("--kernel", type=int, default=0,
                    help="fs_ctx_set_kernel variant: 0 automatic, 2 mixed-length, 4 one-pass")
+    p.add_argument("--region-clocks", default=None, metavar="PATH",
+                   help="measurement aid: write the timed region's CLOCK_MONOTONIC / CLOCK_BOOTTIME stamps (t0, "
+                        "each step's return, t1) to PATH as JSON, to line them up with a rocprofv3 trace "
+                        "(tools/region_attr.py)")
+    p.add_argument("--no-sub", action="store_true",
+                   help="N=1 C2: skip the C3 and C5 sub-records of the line (BASELINE configs[2], [4])")
     p.add_argument("--streams", type=int, default=5,
                    help="HIP streams the steps rotate over: step i+1's kernel starts on the CUs step i's "
                         "tail frees (every batch is still fully digested). 5 measured best on the 4 hardware "
@@ -167,7 +175,17 @@ def make_batch(cfg: str, n: int, seed: int):
         return synth.uniform_batch(n, 1500, seed=seed)
     if cfg == "c5":
         return synth.uniform_batch(n, 9000, seed=seed)
+    if cfg == "small":
+        return synth.hello_batch(n, seed=seed)
     return synth.mixed_batch(n, seed=seed)
+
+
+WORKLOADS = {
+    "c2": "C2: 65536 x 1500-B TCP frames per GPU (BASELINE configs[1])",
+    "c3": "C3: 65536 mixed 64/576/1500/9000-B TCP/UDP frames per GPU (BASELINE configs[2])",
+    "small": "the reference's benchmark shape (stacks/benchmark_test.go:12-46): 65536 x 47-B UDP 'hello' frames "
+             "per GPU in 48-B slots",
+}
 
 
 def box_cores() -> int:
@@ -253,7 +271,7 @@ def cpu_rate(cfg: str, seconds: float, threads: int):
 def cpu_baseline(cfg: str, seconds: float, threads: int):
     """All-cores figure (the box's CPU share) with the 1-thread figure beside it."""
     threads = threads or box_cores()
-    what = {"c2": "1500-B TCP", "c4": "1500-B TCP", "c5": "9000-B TCP"}.get(cfg, "mixed")
+    what = {"c2": "1500-B TCP", "c4": "1500-B TCP", "c5": "9000-B TCP", "small": "47-B UDP 'hello'"}.get(cfg, "mixed")
     v1, r1, nbytes, e1 = cpu_rate(cfg, seconds / 2, 1)
     vn, rn, _, en = cpu_rate(cfg, seconds / 2, threads)
     return {
@@ -446,15 +464,23 @@ def main():
         dist.barrier()
     GPU.sync()
     gc.disable()
+    rc = region_clocks_begin(args.region_clocks)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, i, args.steps)
+        if rc is not None:
+            rc["steps"].append(time.clock_gettime_ns(time.CLOCK_MONOTONIC))
+    if rc is not None:
+        rc["enqueued"] = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     drain()
     GPU.settle(streams + ([xfer] if gather else []))
+    if rc is not None:
+        rc["settled"] = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     GPU.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    region_clocks_end(rc, args.region_clocks, elapsed)
     gc.enable()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -504,15 +530,14 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "frames_per_s": round(n * args.steps * world / elapsed, 1),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": f"synthetic: {nb} distinct resident batches ({resident / 1e6:.0f} MB) of valid frames, rotated",
             "config": {
-                "workload": ("C2: 65536 x 1500-B TCP frames per GPU (BASELINE configs[1])" if args.config == "c2"
-                             else "C3: 65536 mixed 64/576/1500/9000-B TCP/UDP frames per GPU (BASELINE configs[2])")
-                if n == 65536 else f"{args.config} with {n} frames per GPU",
+                "workload": WORKLOADS[args.config] if n == 65536 else f"{args.config} with {n} frames per GPU",
                 "frames_per_gpu": n,
                 "bytes_per_gpu_step": bytes_per_batch,
                 "global_batch_frames": n * world,
@@ -548,6 +573,10 @@ def main():
                 "kernel_avg_us": round(k_avg_ms * 1e3, 3),
                 "kernel_timing": "HIP events around K back-to-back launches on the launch stream",
                 "algorithmic_bytes_per_launch": bytes_per_batch,
+                # per frame the kernel also reads its 12-B descriptor (offset, length) and writes its
+                # 9-B result (digest, verdict): not algorithmic bytes, but 45% of them at 47-B frames
+                "metadata_bytes_per_launch": 21 * n,
+                "achieved_incl_metadata": round((bytes_per_batch + 21 * n) / (k_avg_ms * 1e-3) / 1e9, 1),
             },
             "cpu_baseline": cpu,
         }
@@ -555,6 +584,14 @@ def main():
     del batches, flat
     if gather:
         del rbuf, rviews, recv
+    if rank == 0 and world == 1 and args.config == "c2" and args.op == "digest" and not args.no_sub:
+        # BASELINE configs[2] and [4] beside the C2 headline: the C3
+        # mixed batch device-resident (same steps and warmup) and the C5 jumbo batch end to end
+        # from pinned host memory; each bounded to a few seconds
+        GPU.empty_cache()
+        result["c3"] = sub_record_c3(args, dev)
+        GPU.empty_cache()
+        result["c5_host"] = sub_record_c5(args)
     if world > 1 and args.config == "c2" and args.op == "digest" and not args.no_c4:
         # the C4 strong-scaled record beside the weak-scaled C2 value (same steps / warmup)
         GPU.empty_cache()
@@ -567,6 +604,144 @@ def main():
     if dist.is_initialized():
         dist.destroy_process_group()
     return result
+
+
+def single_gpu_region(engine, batches, steps: int, warmup: int, min_warm: int, ns: int, dev):
+    """The N = 1 step loop of main() without the gather: prewarm over the streams, host spin,
+    warmup steps, then K timed steps (barrier-free: one rank) closed by a polled settle and a
+    synchronize; then K back-to-back launches on one stream between HIP events. Returns
+    (elapsed seconds of the K steps, average kernel ms)."""
+    import torch
+
+    n = int(batches[0][2].numel())
+    nslot = max(2, ns)
+    slab = (9 * n + 255) // 256 * 256
+    flat = torch.empty(nslot * slab, dtype=torch.uint8, device=dev)
+    outs = [flat[k * slab: k * slab + 8 * n].view(torch.int32).view(n, 2) for k in range(nslot)]
+    stats = [flat[k * slab + 8 * n: k * slab + 9 * n] for k in range(nslot)]
+    streams = [GPU.stream(dev) for _ in range(ns)]
+    nb = len(batches)
+
+    def launch(i, s):
+        fb, fo, fl = batches[i % nb]
+        engine.digest_device(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=s)
+
+    for i in range(max(0, min_warm - warmup)):
+        launch(i, streams[i % ns])
+    GPU.settle(streams)
+    GPU.sync()
+    gc.collect()
+    host_warm()
+    for i in range(warmup):
+        launch(i, streams[i % ns])
+    GPU.settle(streams)
+    GPU.sync()
+    gc.disable()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        launch(warmup + i, streams[i % ns])
+    GPU.settle(streams)
+    GPU.sync()
+    elapsed = time.perf_counter() - t0
+    gc.enable()
+    k0, k1 = GPU.event(), GPU.event()
+    with GPU.use(streams[0]):
+        k0.record(streams[0])
+        for i in range(steps):
+            launch(i, streams[0])
+        k1.record(streams[0])
+    GPU.sync()
+    return elapsed, k0.elapsed_time(k1) / steps
+
+
+def sub_record_c3(args, dev):
+    """C3 (BASELINE configs[2]) device-resident beside the C2 headline: 65,536 mixed
+    64/576/1500/9000-B frames, 2 resident batches (365 MB, past the 256 MiB Infinity Cache),
+    the automatic kernel choice (the mixed-length kernel for this batch), the same steps and
+    warmup as the headline."""
+    import torch
+
+    engine = GPU.engine(0)
+    t_start = time.perf_counter()
+    batches = []
+    for b in range(2):
+        buf, off, ln = make_batch("c3", 65536, seed=301 + b)
+        batches.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)))
+    nbytes = int(batches[0][2].sum().item())
+    elapsed, k_ms = single_gpu_region(engine, batches, args.steps, args.warmup, args.min_warm, max(1, args.streams), dev)
+    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a"}.get(engine.last_kernel())
+    engine.close()
+    del batches
+    return {
+        "workload": WORKLOADS["c3"],
+        "value": round(nbytes * args.steps / elapsed / GIB, 3),
+        "unit": "GiB/s",
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "bytes_per_step": nbytes,
+        "kernel_avg_us": round(k_ms * 1e3, 3),
+        "frac": round(nbytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "frac_whole_job": round(nbytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+        "kernel_chosen": chosen,
+        "note": "whole-job value over the same steps/warmup and streams as the headline; frac = algorithmic "
+                "bytes / kernel_avg_us (HIP events around K back-to-back launches on one stream) / 8 TB/s",
+        "wall_s": round(time.perf_counter() - t_start, 2),
+    }
+
+
+def sub_record_c5(args, steps: int = 10, warmup: int = 3):
+    """C5 (BASELINE configs[4]) on one GPU beside the headline: 16,384 x 9000-B jumbo frames from
+    pinned host memory through fs_digest_batch_multi (one context), results back in host memory;
+    PCIe-inclusive, never the headline value."""
+    from seqs_amd import Engine, digest_host_multi
+
+    t_start = time.perf_counter()
+    eng = Engine(0)
+    src, off, ln = make_batch("c5", 16384, seed=55)
+    pinned = eng.host_empty(src.shape, np.uint8)
+    pinned[:] = src
+    del src
+    total = int(ln.astype(np.int64).sum())
+    for _ in range(warmup):
+        digest_host_multi([eng], pinned, off, ln)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, st = digest_host_multi([eng], pinned, off, ln)
+    elapsed = time.perf_counter() - t0
+    assert (st == 0).all(), "valid frames must all verify"
+    eng.close()
+    gbs = total / (elapsed / steps) / 1e9
+    return {
+        "workload": "C5 shape on 1 GPU: 16384 x 9000-B jumbo frames streamed from pinned host memory "
+                    "(fs_digest_batch_multi, one context), results back in host memory",
+        "value": round(total * steps / elapsed / GIB, 3),
+        "unit": "GiB/s",
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "bytes_per_step": total,
+        "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": 63.0, "unit": "GB/s",
+                     "frac": round(gbs / 63.0, 4), "note": "PCIe Gen5 x16 spec 63 GB/s (MI355X_MICROARCH.md)"},
+        "wall_s": round(time.perf_counter() - t_start, 2),
+    }
+
+
+def _clocks():
+    return {"mono": time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+            "boot": time.clock_gettime_ns(getattr(time, "CLOCK_BOOTTIME", time.CLOCK_MONOTONIC))}
+
+
+def region_clocks_begin(path):
+    """--region-clocks: the clocks right before t0 (None when not asked for)."""
+    return None if not path else {"t0": _clocks(), "steps": []}
+
+
+def region_clocks_end(rc, path, elapsed):
+    if rc is None:
+        return
+    rc["t1"] = _clocks()
+    rc["elapsed_us"] = elapsed * 1e6
+    with open(path, "a") as f:
+        f.write(json.dumps(rc) + "\n")
 
 
 def host_warm(seconds: float = 3e-3):

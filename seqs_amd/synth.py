@@ -117,3 +117,49 @@ def mixed_batch(n: int, seed: int = 2):
             pos = offsets[idx][:, None] + np.arange(L, dtype=np.int64)[None, :]
             buf[pos.reshape(-1)] = f.reshape(-1)
     return buf, offsets, lengths
+
+
+HELLO_LEN = ETH + IP + UDP + 5  # 47 B
+
+
+def hello_batch(n: int, seed: int = 0, stride: int = 48):
+    """The reference's own benchmark shape (stacks/benchmark_test.go:12-46, 67-98): UDP frames
+    carrying the 5-byte payload "hello" (47 B), built as NoisyUDPSource.WritePacket builds them:
+    Ethernet dst 01:00:00:00:00:00, EtherType IPv4; IPv4 VersionAndIHL 5 (Put writes 0x45,
+    eth/headers.go:289-301), TTL 64, protocol 17, destination 192.168.1.1, total length 33; UDP
+    destination port 67, length 13; valid IPv4 and UDP checksums. randomizeSource's fields come
+    from one 63-bit value per frame (Ethernet source = its 6 low bytes, IPv4 source = its 4 low
+    bytes, UDP source port = bits 32..47, IP ID = low16 ^ bits 16..31), drawn here from numpy's
+    PRNG, not Go's math/rand (seed 0). Frames sit `stride` bytes apart (48: dword-aligned slots)."""
+    if stride < HELLO_LEN:
+        raise ValueError("stride below the frame length")
+    rng = np.random.default_rng(seed)
+    v = rng.integers(0, 1 << 63, size=n, dtype=np.int64).astype(np.uint64)
+    b = lambda k: ((v >> np.uint64(8 * k)) & np.uint64(0xFF)).astype(np.uint8)  # noqa: E731
+    f = np.zeros((n, HELLO_LEN), np.uint8)
+    f[:, 0] = 0x01
+    for k in range(6):
+        f[:, 6 + k] = b(k)
+    f[:, 12], f[:, 13] = 0x08, 0x00
+    f[:, 14] = 0x45
+    _put16(f, 16, np.full(n, IP + UDP + 5, np.uint32))
+    ipid = ((v & np.uint64(0xFFFF)) ^ ((v >> np.uint64(16)) & np.uint64(0xFFFF))).astype(np.uint32)
+    _put16(f, 18, ipid)
+    f[:, 22] = 64
+    f[:, 23] = 17
+    for k in range(4):
+        f[:, 26 + k] = b(k)
+    f[:, 30:34] = (192, 168, 1, 1)
+    _put16(f, 24, _fold_not(_be_word_sum(f[:, 14:34])))
+    sport = ((v >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.uint32)
+    _put16(f, 34, sport)
+    _put16(f, 36, np.full(n, 67, np.uint32))
+    _put16(f, 38, np.full(n, UDP + 5, np.uint32))
+    f[:, 42:47] = np.frombuffer(b"hello", np.uint8)
+    pseudo = _be_word_sum(f[:, 26:34]) + np.uint64(17) + np.uint64(UDP + 5)
+    _put16(f, 40, _fold_not(_be_word_sum(f[:, 34:]) + pseudo))
+    buf = np.zeros(n * stride + 16, np.uint8)
+    buf[: n * stride].reshape(n, stride)[:, :HELLO_LEN] = f
+    offsets = np.arange(n, dtype=np.int64) * stride
+    lengths = np.full(n, HELLO_LEN, dtype=np.int32)
+    return buf, offsets, lengths
