@@ -69,76 +69,126 @@ var verdictErr = [...]error{
 	eth.VerdictChecksum:           ErrChecksumTCPorUDP,
 }
 
+// gateKind is one step of RecvEth's decision order (portstack.go:163-355) once the GPU has
+// evaluated a frame's byte-level gates. recvEthVerified walks recvEthGates in order; the order
+// and the verdict classes each step ends the frame on are data, so that
+// tests/test_go_gate_order.py reads this table from this file and checks it, for every verdict
+// and every stack state (MAC filter, IP filter, open sockets), against a transliteration of
+// RecvEth's branches.
+type gateKind uint8
+
+const (
+	gateLength    gateKind = iota // :167-172 frame length < 34 -> errPacketSmol; > MTU -> errPacketExceedsMTU
+	gateGlobal                    // :178-184 the stack's global handler (its error ends the frame)
+	gateMAC                       // :186-187 destination MAC neither broadcast nor ours -> nil
+	gateEtherType                 // :187-197 not IPv4 or ARP -> nil; ARP: length gate, then the ARP client
+	gateVerdict                   // the GPU verdict ends the frame when it is one of the step's classes
+	gateIPDest                    // :209-210 IP destination neither ours nor our address unset -> nil
+	gateSockets                   // :223, :284 no socket of the frame's protocol -> nil
+	gateDeliver                   // :246-281 UDP, :309-346 TCP: the segment to its port's handler
+)
+
+type gate struct {
+	kind    gateKind
+	classes []eth.Verdict // gateVerdict: the verdicts that end the frame at this step
+	logged  bool          // gateVerdict: RecvEth logs the error (the protocol switch, :348-350)
+}
+
+// recvEthGates is RecvEth's branch order (portstack.go:163-355) around the GPU verdict.
+var recvEthGates = [...]gate{
+	{kind: gateLength},
+	{kind: gateGlobal},
+	{kind: gateMAC},
+	{kind: gateEtherType},
+	{kind: gateVerdict, classes: []eth.Verdict{eth.VerdictIPVersion, eth.VerdictInvalidIHL}},
+	{kind: gateIPDest},
+	{kind: gateVerdict, classes: []eth.Verdict{eth.VerdictBadIPTotalLenOrIHL, eth.VerdictExceedsMTU}},
+	{kind: gateVerdict, classes: []eth.Verdict{eth.VerdictUnknownIPProto}, logged: true},
+	{kind: gateSockets},
+	{kind: gateVerdict, classes: []eth.Verdict{eth.VerdictTooShortTCPOrUDP, eth.VerdictZeroPort, eth.VerdictBadUDPLength, eth.VerdictBadTCPOffset, eth.VerdictChecksum}, logged: true},
+	{kind: gateDeliver},
+}
+
 // recvEthVerified finishes one frame whose byte-level gates and L4 checksum the GPU has
 // evaluated (verdict v). The GPU applies RecvEth's gates in RecvEth's order under a fixed
-// stack model (no MAC / IP destination filter, sockets open); here the stack-state
-// branches are put back at the point where RecvEth takes them, so a verdict only counts
-// once the frame has got that far.
+// stack model (no MAC / IP destination filter, sockets open); the steps of recvEthGates put
+// the stack-state branches back at the point where RecvEth takes them, so a verdict only
+// counts once the frame has got that far.
 func (ps *PortStack) recvEthVerified(frame []byte, v eth.Verdict) error {
-	// The length gates come before anything else (:167-172).
-	if len(frame) < eth.SizeEthernetHeader+eth.SizeIPv4Header {
-		return errPacketSmol
-	} else if len(frame) > int(ps.mtu) {
-		return errPacketExceedsMTU
-	}
-	ps.trace("Stack.RecvEth:start", slog.Int("plen", len(frame)))
-	ps.lastRx = ps.now()
-	ps.auxEth = eth.DecodeEthernetHeader(frame)
-	ehdr := &ps.auxEth
-	if ps.glob != nil {
-		if err := ps.glob(ehdr, frame[eth.SizeEthernetHeader:]); err != nil {
+	var (
+		ehdr     *eth.EthernetHeader
+		ihdr     eth.IPv4Header
+		ipOffset uint8
+	)
+	for _, g := range recvEthGates {
+		switch g.kind {
+		case gateLength:
+			if len(frame) < eth.SizeEthernetHeader+eth.SizeIPv4Header {
+				return errPacketSmol
+			} else if len(frame) > int(ps.mtu) {
+				return errPacketExceedsMTU
+			}
+			ps.trace("Stack.RecvEth:start", slog.Int("plen", len(frame)))
+			ps.lastRx = ps.now()
+			ps.auxEth = eth.DecodeEthernetHeader(frame)
+			ehdr = &ps.auxEth
+		case gateGlobal:
+			if ps.glob != nil {
+				if err := ps.glob(ehdr, frame[eth.SizeEthernetHeader:]); err != nil {
+					return err
+				}
+			}
+		case gateMAC:
+			if ehdr.Destination != eth.BroadcastHW6() && ehdr.Destination != ps.mac {
+				return nil
+			}
+		case gateEtherType:
+			switch ehdr.AssertType() {
+			case eth.EtherTypeARP:
+				if v == eth.VerdictPacketSmol { // the ARP length gate (:192-194)
+					return errPacketSmol
+				}
+				ps.auxARP = eth.DecodeARPv4Header(frame[eth.SizeEthernetHeader:])
+				return ps.arpClient.recv(&ps.auxARP)
+			case eth.EtherTypeIPv4:
+				ihdr, ipOffset = eth.DecodeIPv4Header(frame[eth.SizeEthernetHeader:])
+			default:
+				return nil
+			}
+		case gateVerdict:
+			for _, c := range g.classes {
+				if v == c {
+					err := verdictErr[v]
+					if g.logged && err != nil {
+						ps.error("Stack.RecvEth", slog.String("err", err.Error()))
+					}
+					return err
+				}
+			}
+		case gateIPDest:
+			if ps.ip != ihdr.Destination && ps.ip != [4]byte{} {
+				return nil
+			}
+		case gateSockets:
+			if (ihdr.Protocol == 17 && len(ps.portsUDP) == 0) || (ihdr.Protocol == 6 && len(ps.portsTCP) == 0) {
+				return nil // RecvEth stops before its L4 gates
+			}
+		case gateDeliver:
+			offset := eth.SizeEthernetHeader + int(ipOffset)
+			segment := frame[offset : eth.SizeEthernetHeader+int(ihdr.TotalLength)]
+			var err error
+			if ihdr.Protocol == 17 {
+				err = ps.deliverUDP(ehdr, &ihdr, segment)
+			} else {
+				err = ps.deliverTCP(ehdr, &ihdr, frame[eth.SizeEthernetHeader+eth.SizeIPv4Header:offset], segment)
+			}
+			if err != nil {
+				ps.error("Stack.RecvEth", slog.String("err", err.Error()))
+			}
 			return err
 		}
 	}
-	// Destination MAC and EtherType filters (:185-189).
-	if ehdr.Destination != eth.BroadcastHW6() && ehdr.Destination != ps.mac {
-		return nil
-	}
-	switch ehdr.AssertType() {
-	case eth.EtherTypeARP: // (:191-197) the only gate is the ARP length
-		if v == eth.VerdictPacketSmol {
-			return errPacketSmol
-		}
-		ps.auxARP = eth.DecodeARPv4Header(frame[eth.SizeEthernetHeader:])
-		return ps.arpClient.recv(&ps.auxARP)
-	case eth.EtherTypeIPv4:
-	default:
-		return nil
-	}
-	ihdr, ipOffset := eth.DecodeIPv4Header(frame[eth.SizeEthernetHeader:])
-	// Version and IHL come before the IP destination filter, the length and MTU gates after
-	// it (:203-215).
-	if v == eth.VerdictIPVersion || v == eth.VerdictInvalidIHL {
-		return verdictErr[v]
-	}
-	if ps.ip != ihdr.Destination && ps.ip != [4]byte{} {
-		return nil
-	}
-	if v == eth.VerdictBadIPTotalLenOrIHL || v == eth.VerdictExceedsMTU {
-		return verdictErr[v]
-	}
-	// The protocol switch (:218-347): its errors are the ones RecvEth logs.
-	var err error
-	switch {
-	case v == eth.VerdictUnknownIPProto:
-		err = verdictErr[v]
-	case (ihdr.Protocol == 17 && len(ps.portsUDP) == 0) || (ihdr.Protocol == 6 && len(ps.portsTCP) == 0):
-		// no socket of the frame's protocol: RecvEth stops before its L4 gates (:223, :284)
-	case v != eth.VerdictOK:
-		err = verdictErr[v]
-	default: // verified: hand the segment to its socket (:246-281 UDP, :309-346 TCP)
-		offset := eth.SizeEthernetHeader + int(ipOffset)
-		segment := frame[offset : eth.SizeEthernetHeader+int(ihdr.TotalLength)]
-		if ihdr.Protocol == 17 {
-			err = ps.deliverUDP(ehdr, &ihdr, segment)
-		} else {
-			err = ps.deliverTCP(ehdr, &ihdr, frame[eth.SizeEthernetHeader+eth.SizeIPv4Header:offset], segment)
-		}
-	}
-	if err != nil {
-		ps.error("Stack.RecvEth", slog.String("err", err.Error()))
-	}
-	return err
+	return nil
 }
 
 // deliverUDP passes a verified UDP datagram to the port listening on its destination port.

@@ -6,12 +6,15 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r4a; mkdir -p $O
+if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 180 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/tests.log | head -20; exit 1; }
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-/usr/bin/time -f "%e s wall" -o $O/driver.wall timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/driver.json 2> $O/driver.err || { echo FAIL driver; tail -5 $O/driver.err; exit 1; }
-cat $O/driver.wall
+fi
+T0=$(date +%s.%N)
+timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/driver.json 2> $O/driver.err || { echo FAIL driver; tail -5 $O/driver.err; exit 1; }
+python3 -c "import sys,time; print('driver command wall %.1f s' % (time.time() - float(sys.argv[1])))" $T0
 python - <<'EOF'
 import json
 d = json.loads(open("gpurun_out/r4a/driver.json").read().strip().splitlines()[-1])
@@ -37,4 +40,6 @@ timeout -k 10 240 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $O
 python3 tools/region_attr.py $O/rtrace $O/clk.json | tee $O/region_attr.txt
 # keep the small CSVs only (the API trace of the whole run is large)
 find $O/rtrace -name "*hip_api_trace.csv" -size +20M -delete
+timeout -k 10 120 tools/tile_pattern w4 > $O/tile_pattern_w4.log 2>&1 || { echo FAIL tile_pattern; tail -3 $O/tile_pattern_w4.log; exit 1; }
+cat $O/tile_pattern_w4.log
 echo done

@@ -44,7 +44,11 @@ __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ 
     const uint32_t nwaves = gridDim.x * WPB;
     const uint32_t ntiles = (nframes + FPT - 1) / FPT;
     const uint32_t my_tiles = gwave < ntiles ? (ntiles - gwave + nwaves - 1) / nwaves : 0;
-    const int Rmax = AL ? (int)((flen + RB - 1) / RB + 1) : (int)((flen + RB - 1) / RB);
+    // AL 4 (G = 16): 256-B rows of 4 whole 64-B blocks, the last row ending with the frame's last
+    // block (the one-pass kernel's block-aligned rows, 4 blocks per row); blocks before the frame's
+    // first block reload that block's chunk, as the kernel's clamped loads do
+    const int Rmax = AL == 4 ? (int)(((flen + 63) / 64 + 1 + 3) / 4)
+                     : AL ? (int)((flen + RB - 1) / RB + 1) : (int)((flen + RB - 1) / RB);
     const int nq = (int)my_tiles * Rmax;
     // address of flattened row q for this lane; false if the lane loads nothing
     auto addr = [&](int q, const u32x4_a4*& p) -> bool {
@@ -53,7 +57,11 @@ __global__ void __launch_bounds__(64 * WPB) k_tiles(const uint8_t* __restrict__ 
         if (f >= nframes) return false;
         const uint64_t S = (uint64_t)f * flen, E = S + flen;
         uint64_t a;
-        if (AL) {
+        if (AL == 4) {
+            const int64_t b0 = (int64_t)(S / 64), b1 = (int64_t)((E - 1) / 64);
+            const int64_t b = b1 - 4 * (Rmax - 1 - r) - 3 + (int64_t)(gl >> 2);
+            a = (uint64_t)(b < b0 ? b0 : b) * 64u + 16u * (gl & 3u);
+        } else if (AL) {
             const uint64_t b0 = S / RB, b1 = (E - 1) / RB;
             if (b0 + (uint64_t)r > b1) return false;
             // AL 3: whole blocks, the odd groups' frames read backwards (last block first), so the
@@ -320,11 +328,11 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    if (argc > 1 && std::string(argv[1]) == "map") {
 #define TILESM(G, PF, AL, MAP)                                                                             \
     run([&](int i, hipStream_t s) {                                                                       \
         hipLaunchKernelGGL((k_tiles<G, PF, AL, 16, MAP>), dim3(cus), dim3(1024), 0, s, bufs[i % NB], nf, flen, out); \
     }, "tiles G=" #G " PF=" #PF " AL=" #AL " MAP=" #MAP)
+    if (argc > 1 && std::string(argv[1]) == "map") {
         for (int rep = 0; rep < 2; ++rep) {
             STREAM(4, 16, 1);
             TILESM(4, 5, 2, 0);
@@ -332,6 +340,22 @@ int main(int argc, char** argv) {
             TILESM(16, 6, 0, 1);
             TILESM(16, 5, 0, 0);
             TILESM(16, 5, 0, 1);
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "w4") {
+        // round 4: 16 lanes per frame with rows of 4 whole 64-B blocks end-anchored at the frame's
+        // last block (AL 4), against the one-pass kernel's pattern and 256-B end-anchored rows
+        for (int rep = 0; rep < 2; ++rep) {
+            STREAM(4, 16, 1);
+            TILESM(4, 5, 2, 0);
+            TILESM(16, 6, 0, 0);
+            TILESM(16, 5, 4, 0);
+            TILESM(16, 6, 4, 0);
+            TILESM(16, 7, 4, 0);
+            TILESM(16, 8, 4, 0);
+            TILESM(16, 7, 4, 1);
+            TILESM(16, 7, 2, 0);
         }
         return 0;
     }
