@@ -92,8 +92,11 @@ class GpuOps:
             e = torch.cuda.Event()
             e.record(s)
             evs.append(e)
-        while not all(e.query() for e in evs):
-            pass
+        # one event at a time, the last-launched stream's last: once the last kernel ends the loop
+        # sees it within one query (a sweep over every event per iteration took ~5 queries to notice)
+        for e in evs:
+            while not e.query():
+                pass
 
     def mark(self, s):
         """an event recorded on stream s now (a dependency marker, no timing)"""
@@ -473,7 +476,8 @@ def main():
     if rc is not None:
         rc["enqueued"] = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     drain()
-    GPU.settle(streams + ([xfer] if gather else []))
+    # (in launch order: the stream of the region's last step is polled last)
+    GPU.settle([streams[(args.steps + t) % ns] for t in range(ns)] + ([xfer] if gather else []))
     if rc is not None:
         rc["settled"] = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     GPU.sync()

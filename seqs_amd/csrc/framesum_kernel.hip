@@ -1632,7 +1632,11 @@ constexpr uint32_t kW2Cells = 9;       // slot cells: frame dwords [0, 33) at an
 constexpr uint32_t kW2HdrStride = kW2Cells * 256u;
 constexpr uint32_t kW2Hdr = kW2Region + 65536;
 constexpr uint32_t kW2Park = kW2Hdr + kWavesPerBlock * kW2HdrStride;  // per wave: 16 frames x {Y, csum}
-constexpr uint32_t kW2LdsBytes = kW2Park + kWavesPerBlock * 128u;
+// per wave: the descriptors of two tiles (the current one and the next, alternating), written by
+// LDS-DMA as [field: S lo, S hi, len][group] dwords, so no VGPR holds them across the rows
+constexpr uint32_t kW2Desc = kW2Park + kWavesPerBlock * 128u;
+constexpr uint32_t kW2DescStride = 2u * 192u;
+constexpr uint32_t kW2LdsBytes = kW2Desc + kWavesPerBlock * kW2DescStride;
 static_assert(kW2LdsBytes <= kLdsBytes, "the 16-lane kernel's LDS map fits the shared array");
 static_assert(kW2Region < 65536, "region W's base folds into the ds_read offset field");
 static_assert(kW2Zfin + 16384 == kW2Region, "48 plain pieces before region W");
@@ -1713,12 +1717,12 @@ __device__ __forceinline__ void wait_row(u32x4& v) {
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "n"(N));
 }
 
-// A sub-tile in the 16-lane layout: the lane's frame (of its 4-lane group 4 s + fj, by
-// ds_bpermute from that group's lane 0) and where its rows are.
+// A sub-tile in the 16-lane layout: the lane's frame (group 4 s + fj of the tile, from the LDS
+// descriptor table) and where its rows are.
 struct SubW {
-    const uint32_t* fb;  // frame dword 0 (an empty lane: the tables, a valid address)
-    int x00;             // frame dword of this lane's chunk in row 0
-    int nd;              // stream dwords (0: empty lane or a frame under 4 bytes)
+    const uint32_t* fb;  // frame dword 0 of the lane's loads (an empty lane: a longest frame's)
+    int x00;             // frame dword of this lane's chunk in row 0 (of the loads' frame)
+    int nd;              // own stream dwords (0: empty lane or a frame under 4 bytes)
     int lo;              // lowest frame dword a clamped load may start at
     uint32_t sat;        // S & 3 | tail mask bytes << 2 (te, 1..4)
     int P;               // wave-uniform: rows (a multiple of kRingW; 0: nothing to stream)
@@ -1726,38 +1730,38 @@ struct SubW {
     int Hc;              // wave-uniform: leading rows holding slot cells (frame dwords < 36)
 };
 
-__device__ __forceinline__ int wave_max(int x) {
-    x = max(x, __builtin_amdgcn_mov_dpp(x, 0x140, 0xf, 0xf, false));  // row_mirror
-    x = max(x, __builtin_amdgcn_mov_dpp(x, 0x141, 0xf, 0xf, false));  // row_half_mirror
-    x = max(x, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, false));   // quad [1,0,3,2]
-    const int a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
-    const int c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
-    return max(max(a, b), max(c, d));
+// The 4 frames of a sub-tile sit in the wave's 4 rows of 16 lanes, one frame per row: a wave
+// max of a frame value is a max over 4 readlanes.
+__device__ __forceinline__ int rows_max(int x) {
+    return max(max(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+               max(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
 }
 
-__device__ __forceinline__ SubW sub_state(int s, uint32_t fj, uint32_t ch, uint64_t S, uint32_t len,
+// sub-tile state from the descriptor table `dt` (LDS byte address) of a tile whose frame of group
+// g is valid when bit g of `vmask` is set (kOpsFcs: the rows stream the frame without its FCS)
+template <uint32_t kOps>
+__device__ __forceinline__ SubW sub_state(int s, uint32_t fj, uint32_t ch, uint32_t dt, uint32_t vmask,
                                           const uint8_t* __restrict__ frames) {
     SubW R;
-    const int src = (int)((16u * (uint32_t)s + 4u * fj) << 2);
-    const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)S);
-    const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(S >> 32));
-    const uint32_t ln = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
+    const char* lds = g_lds;
+    const uint32_t g = 4u * (uint32_t)s + fj;
+    const uint32_t slo = lds32(lds, dt + 4u * g), shi = lds32(lds, dt + 64u + 4u * g);
+    uint32_t ln = ((vmask >> g) & 1u) ? lds32(lds, dt + 128u + 4u * g) : 0u;
+    if (kOps == kOpsFcs) ln = ln >= 4u ? ln - 4u : 0u;
     const uint32_t sa = slo & 3u;
     R.nd = ln >= 4u ? (int)((sa + ln + 3u) >> 2) : 0;
     const int rows = (R.nd + 63) >> 6;
-    const int Rx = wave_max(rows);
+    const int Rx = rows_max(rows);
     R.P = (Rx + kRingW - 1) / kRingW * kRingW;
     const uint32_t e = (sa + ln) & 3u;
     R.sat = sa | ((e ? e : 4u) << 2);
-    const uint64_t sdw = (((uint64_t)shi << 32) | slo) >> 2;
+    uint64_t ld_sdw = (((uint64_t)shi << 32) | slo) >> 2;
     int ld_nd = R.nd;
-    uint64_t ld_sdw = sdw;
     {   // an empty lane loads the chunks of a longest frame of the sub-tile (its own results are
         // discarded), so that every row load stays inside a frame
-        const uint64_t ball = __ballot(rows == Rx);
-        const int srcl = (int)__builtin_ctzll(ball);
-        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sdw, srcl);
-        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sdw >> 32), srcl);
+        const int srcl = (int)__builtin_ctzll(__ballot(rows == Rx));
+        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ld_sdw, srcl);
+        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ld_sdw >> 32), srcl);
         const int s_nd = __builtin_amdgcn_readlane(R.nd, srcl);
         if (R.nd == 0) {
             ld_sdw = ((uint64_t)s_hi << 32) | s_lo;
@@ -1770,10 +1774,10 @@ __device__ __forceinline__ SubW sub_state(int s, uint32_t fj, uint32_t ch, uint6
     // masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
     // dword before the frame (chunk 0 holds the row's lowest dword)
     const int need = 2 - (R.nd - 64 * R.P);
-    R.H = wave_max(R.nd > 0 && need > 0 ? min((need + 63) >> 6, R.P) : 0);
+    R.H = rows_max(R.nd > 0 && need > 0 ? min((need + 63) >> 6, R.P) : 0);
     // slot cells: rows up to the one holding frame dword 35
     const int need_c = 36 - (R.nd - 64 * R.P);
-    R.Hc = wave_max(R.nd > 0 ? min((need_c + 63) >> 6, R.P) : 0);
+    R.Hc = rows_max(R.nd > 0 ? min((need_c + 63) >> 6, R.P) : 0);
     return R;
 }
 
@@ -1805,6 +1809,14 @@ __device__ __forceinline__ u32x4 masked_row_w2(const char* lds, const LaneKeys& 
     return u32x4{v[0], v[1], v[2], v[3]};
 }
 
+// The lane index from mbcnt, opaque to the compiler: values derived from it are recomputed where
+// they are used instead of being hoisted into registers held by the whole kernel.
+__device__ __forceinline__ uint32_t lane_id_opaque() {
+    uint32_t ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    return ln;
+}
+
 template <uint32_t kOps>
 __global__ void __launch_bounds__(kThreads, 1)
 digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
@@ -1816,13 +1828,13 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     char* lds = g_lds;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t grp = lane >> 2, gl = lane & 3u;  // 4-lane layout: group 4 s + f
-    const uint32_t fj = lane >> 4, ch = lane & 15u;  // 16-lane layout: frame fj of the sub-tile, chunk ch
+    // (lane-derived indices are recomputed where used: lane_id_opaque)
     const uint32_t NW = gridDim.x * kWavesPerBlock;
     const uint32_t gw = first_tile(wave);
     const uint32_t nq = (n + 3u) / 4u;
     const uint32_t hw = __builtin_amdgcn_readfirstlane(kW2Hdr + wave * kW2HdrStride);
     const uint32_t pk = __builtin_amdgcn_readfirstlane(kW2Park + wave * 128u);
+    const uint32_t dsc = __builtin_amdgcn_readfirstlane(kW2Desc + wave * kW2DescStride);
     LaneKeys keys;
     {
         const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
@@ -1835,32 +1847,44 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             keys.sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
         }
     }
-    // tile j's frame of group g (4-lane layout): quad gw + NW (4 j + g / 4), frame g % 4 of it
+    // tile j's frame of group g (4-lane layout): frame g % 4 of quad gw + NW (4 j + g / 4)
     auto quad_of = [&](uint32_t j, uint32_t g) { return gw + NW * (4u * j + (g >> 2)); };
-    auto tile_valid = [&](uint32_t j) { return __builtin_amdgcn_readfirstlane(quad_of(j, 0)) < nq; };
-    // descriptors of tile j (4-lane layout), issued by inline asm (descriptors_ready waits)
-    auto issue_desc = [&](uint32_t j, uint64_t& S, uint32_t& len, uint32_t& fi) {
-        const uint32_t q = quad_of(j, grp);
-        fi = q < nq ? 4u * q + (grp & 3u) : n;
-        tile_descriptors(0, 0, n, offsets + (fi < n ? fi : n - 1u), lengths + (fi < n ? fi : n - 1u), S, len, 1);
+    auto frame_of = [&](uint32_t j, uint32_t g) {
+        const uint32_t q = quad_of(j, g);
+        return q < nq ? 4u * q + (g & 3u) : n;  // n: no frame
+    };
+    auto tile_valid = [&](uint32_t j) { return quad_of(j, 0) < nq; };
+    // bit g: tile j's group g has a frame (wave-uniform)
+    auto valid_mask = [&](uint32_t j) {
+        uint32_t m = 0;
+        for (uint32_t g = 0; g < 16u; ++g) m |= (frame_of(j, g) < n ? 1u : 0u) << g;
+        return __builtin_amdgcn_readfirstlane(m);
+    };
+    // tile j's descriptors into table buffer b by LDS-DMA (lanes < 16: group = lane)
+    auto issue_desc = [&](uint32_t j, uint32_t b) {
+        const uint32_t lane = lane_id_opaque();
+        const uint32_t f = frame_of(j, lane & 15u);
+        const uint32_t fc = f < n ? f : n - 1u;
+        const uint32_t base = __builtin_amdgcn_readfirstlane(lds_base(lds) + dsc + 192u * b);
+        if (lane < 16u) {
+            dma_x1(reinterpret_cast<const uint32_t*>(offsets + fc), base);
+            dma_x1(reinterpret_cast<const uint32_t*>(offsets + fc) + 1, base + 64u);
+            dma_x1(lengths + fc, base + 128u);
+        }
     };
 
-    uint32_t j = 0;
-    uint64_t S = 0, Sn = 0;
-    uint32_t len = 0, lenn = 0, fi = n, fin = n;
-    const bool first = tile_valid(0);
-    if (first) issue_desc(0, S, len, fi);
-    build_tables_w2(tabs, lds);
-    if (first) {
-        descriptors_ready<kOps>(S, len);
-        if (fi >= n) len = 0u;
-    }
+    const uint32_t* dummy = reinterpret_cast<const uint32_t*>(tabs);
+    u32x4 pf[kRingW];
     SubW cur;
     cur.P = 0;
-    u32x4 pf[kRingW];
-    const uint32_t* dummy = reinterpret_cast<const uint32_t*>(tabs);
+    const bool first = tile_valid(0);
+    if (first) issue_desc(0, 0);
+    build_tables_w2(tabs, lds);
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): tile 0's descriptor table (the only loads so far)
+    uint32_t vm = first ? valid_mask(0) : 0u;
     if (first) {
-        cur = sub_state(0, fj, ch, S, len, frames);
+        const uint32_t l2 = lane_id_opaque();
+        cur = sub_state<kOps>(0, l2 >> 4, l2 & 15u, dsc, vm, frames);
 #pragma unroll
         for (int i = 0; i < kRingW; ++i) {
             const int x = cur.x00 + 64 * i;
@@ -1870,31 +1894,31 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
 #pragma unroll
         for (int i = 0; i < kRingW; ++i) pf[i] = load_row_asm(dummy);
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's table stores (lgkmcnt(0)); the rows stay in flight
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's table stores; the rows stay in flight
     __builtin_amdgcn_s_barrier();
     if ((wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // two-level age priority (as the one-pass kernel)
 
-    while (tile_valid(j)) {
-        const bool more = tile_valid(j + 1);
-        if (more) issue_desc(j + 1, Sn, lenn, fin);  // the next tile's descriptors, one tile ahead
-        const uint32_t sa4 = (uint32_t)S & 3u;       // 4-lane layout: the group's frame
-        const bool parser = fi < n && gl == 0u;
+    for (uint32_t j = 0; tile_valid(j); ++j) {
+        const uint32_t dt = dsc + 192u * (j & 1u);        // this tile's descriptor table
+        const uint32_t dtn = dsc + 192u * ((j + 1u) & 1u);  // the next tile's
+        const bool more = tile_valid(j + 1u);
+        uint32_t vmn = 0u;
         for (int s = 0; s < 4; ++s) {
+            const uint32_t ln = lane_id_opaque();
+            const uint32_t fj = ln >> 4, ch = ln & 15u;
+            if (s == 2 && more) issue_desc(j + 1u, (j + 1u) & 1u);  // ahead of sub-tile 2's refills
             // the refill target after this sub-tile: the next sub-tile, the next tile's first, or nothing
             SubW nxt;
             nxt.P = 0;
-            bool tg = false;
             if (s < 3) {
-                nxt = sub_state(s + 1, fj, ch, S, len, frames);
-                tg = nxt.P > 0;
+                nxt = sub_state<kOps>(s + 1, fj, ch, dt, vm, frames);
             } else if (more) {
-                // the next tile's descriptors are older than the ring's kRingW loads in flight
-                asm volatile("s_waitcnt vmcnt(%2)" : "+v"(Sn), "+v"(lenn) : "n"(kRingW));
-                if (kOps == kOpsFcs) lenn = lenn >= 4u ? lenn - 4u : 0u;
-                if (fin >= n) lenn = 0u;
-                nxt = sub_state(0, fj, ch, Sn, lenn, frames);
-                tg = nxt.P > 0;
+                // the next tile's table: older than the ring's kRingW loads in flight
+                __builtin_amdgcn_s_waitcnt(0x0070 | kRingW);
+                vmn = valid_mask(j + 1u);
+                nxt = sub_state<kOps>(0, fj, ch, dtn, vmn, frames);
             }
+            const bool tg = nxt.P > 0;
             uint32_t A[4] = {0u, 0u, 0u, 0u};
             uint32_t cs = 0u, junk = 0u;
             const int Pc = cur.P / kRingW;
@@ -1930,18 +1954,32 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 if (s == 3 && c == (cur.Hc - 1) / kRingW) {
-                    // ---- header parse of the tile's 16 frames (4-lane layout), all slots captured
+                    // ---- header parse of the tile's 16 frames (4-lane layout), every slot captured
+                    const uint32_t l2 = lane_id_opaque();
+                    const uint32_t grp = l2 >> 2, gl = l2 & 3u;
+                    const uint32_t fi = frame_of(j, grp);
+                    const uint64_t S = ((uint64_t)lds32(lds, dt + 64u + 4u * grp) << 32) | lds32(lds, dt + 4u * grp);
+                    uint32_t len = fi < n ? lds32(lds, dt + 128u + 4u * grp) : 0u;
+                    if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
+                    const uint32_t sa4 = (uint32_t)S & 3u;
                     const uint32_t nd4 = len >= 4u ? (sa4 + len + 3u) >> 2 : 0u;
                     parse_tile<kOps, kHdrDwords>(hw, grp, gl, sa4, len, mtu,
-                                                 reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), parser, hw,
-                                                 (0u - nd4) & 3u);
+                                                 reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
+                                                 fi < n && gl == 0u, hw, (0u - nd4) & 3u);
                 }
             }
             if (s == 3 && cur.P == 0) {  // no rows in the last sub-tile: parse now
+                const uint32_t l2 = lane_id_opaque();
+                const uint32_t grp = l2 >> 2, gl = l2 & 3u;
+                const uint32_t fi = frame_of(j, grp);
+                const uint64_t S = ((uint64_t)lds32(lds, dt + 64u + 4u * grp) << 32) | lds32(lds, dt + 4u * grp);
+                uint32_t len = fi < n ? lds32(lds, dt + 128u + 4u * grp) : 0u;
+                if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
+                const uint32_t sa4 = (uint32_t)S & 3u;
                 const uint32_t nd4 = len >= 4u ? (sa4 + len + 3u) >> 2 : 0u;
                 parse_tile<kOps, kHdrDwords>(hw, grp, gl, sa4, len, mtu,
-                                             reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), parser, hw,
-                                             (0u - nd4) & 3u);
+                                             reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
+                                             fi < n && gl == 0u, hw, (0u - nd4) & 3u);
             }
             // ---- the sub-tile's combine (16-lane layout): the pending register of each frame's
             // last dword, Y = xor over its 64 streams of Z_(4 (63 - p))(A_p), p = 4 ch + j
@@ -1968,16 +2006,21 @@ digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             cur = nxt;
         }
         // ---- finish (4-lane layout): the group's lane 0
-        if (parser) {
-            const uint2 yc = *reinterpret_cast<const uint2*>(lds + pk + 8u * grp);
-            const uint32_t e = (sa4 + len) & 3u;
-            finish_frame<kOps, LayoutW2>(lds, unpark_parsed<kOps>(lds, hw, grp), S, len, e ? e : 4u, yc.x, yc.y, frames,
-                                         wframes, lengths, fi, out, status, tx);
+        {
+            const uint32_t l2 = lane_id_opaque();
+            const uint32_t grp = l2 >> 2, gl = l2 & 3u;
+            const uint32_t fi = frame_of(j, grp);
+            if (fi < n && gl == 0u) {
+                const uint64_t S = ((uint64_t)lds32(lds, dt + 64u + 4u * grp) << 32) | lds32(lds, dt + 4u * grp);
+                uint32_t len = lds32(lds, dt + 128u + 4u * grp);
+                if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
+                const uint2 yc = *reinterpret_cast<const uint2*>(lds + pk + 8u * grp);
+                const uint32_t e = ((uint32_t)S + len) & 3u;
+                finish_frame<kOps, LayoutW2>(lds, unpark_parsed<kOps>(lds, hw, grp), S, len, e ? e : 4u, yc.x, yc.y,
+                                             frames, wframes, lengths, fi, out, status, tx);
+            }
         }
-        ++j;
-        S = Sn;
-        len = lenn;
-        fi = fin;
+        vm = vmn;
     }
 }
 

@@ -11,6 +11,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
 from oracle import coracle  # noqa: E402
 from seqs_amd import Engine, pack_frames, split_digests, synth  # noqa: E402
 
@@ -87,6 +88,28 @@ if __name__ == "__main__":
     ok &= check("random lengths 0-3000", b, o, l)
     b, o, l = synth.hello_batch(65536)
     ok &= check("hello 47-B", b, o, l)
+    # TX fill and FCS verify through the variant
+    from seqs_amd import Engine as _E
+    b, o, l = pack_frames(frames, align=4)
+    import bench
+    b2, o2, l2 = bench.with_room(b, o.astype(np.int64), l.astype(np.int32))
+    exp = b2.copy()
+    edig, est = coracle.fill_batch(exp, o2, l2, 0, 3)
+    e = _E(0)
+    e.set_kernel(VARIANT)
+    tb = torch.from_numpy(b2.copy()).to(dev)
+    out, st = e.fill_device(tb, torch.from_numpy(o2).to(dev), torch.from_numpy(l2).to(dev), flags=3)
+    torch.cuda.synchronize()
+    got = tb.cpu().numpy()
+    fok = np.array_equal(got, exp) and np.array_equal(st.cpu().numpy(), est)
+    print(f"TX fill + FCS append variant {VARIANT}: {'OK' if fok else 'FAIL'}", flush=True)
+    l3 = torch.from_numpy(l2 + 4).to(dev)
+    out, st = e.digest_fcs_device(tb, torch.from_numpy(o2).to(dev), l3)
+    torch.cuda.synchronize()
+    vok = bool((st.cpu().numpy()[est == 0] == 0).all())
+    print(f"FCS verify of the filled frames variant {VARIANT}: {'OK' if vok else 'FAIL'}", flush=True)
+    ok &= fok and vok
+    e.close()
     print("PARITY", "OK" if ok else "FAIL", flush=True)
     if ok and "--time" in sys.argv:
         timing()
