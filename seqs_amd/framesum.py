@@ -268,6 +268,29 @@ class Engine:
         self._check(st, "fs_digest_batch")
         return out, status
 
+    def prepare_digest(self, frames, offsets, lengths, mtu: int = 0, out=None, status=None, stream=None, op="digest"):
+        """A prepared digest_device call: the tensors are checked and the C arguments built ONCE,
+        and the returned callable enqueues the same fs_digest_batch (op "fcs": fs_digest_batch_fcs)
+        again on every call, with no per-call validation or marshalling. For a caller that digests
+        a fixed set of resident batches into fixed result slots over and over (a NIC ring's
+        buffers, the bench's rotated batches): the per-call host cost is the C call alone. The
+        callable keeps the tensors alive and raises FramesumError on a failed call."""
+        n, out, status, stream = self._device_args(frames, offsets, lengths, out, status, stream)
+        name = {"digest": "fs_digest_batch", "fcs": "fs_digest_batch_fcs"}[op]
+        fn = self.lib[name]  # a fresh function pointer with no argtypes: the ctypes objects go as built
+        vp, u32 = ctypes.c_void_p, ctypes.c_uint32
+        args = (vp(self._ctx.value), vp(frames.data_ptr()), vp(offsets.data_ptr()), vp(lengths.data_ptr()), u32(n),
+                u32(mtu), vp(out.data_ptr()), vp(status.data_ptr()), vp(stream.cuda_stream))
+        keep = (frames, offsets, lengths, out, status, stream)
+
+        def call():
+            st = fn(*args)
+            if st:
+                self._check(st, name)
+            return keep[3], keep[4]
+
+        return call
+
     def _device_args(self, frames, offsets, lengths, out, status, stream):
         import torch
 
