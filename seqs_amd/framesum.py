@@ -268,19 +268,22 @@ class Engine:
         self._check(st, "fs_digest_batch")
         return out, status
 
-    def prepare_digest(self, frames, offsets, lengths, mtu: int = 0, out=None, status=None, stream=None, op="digest"):
+    def prepare_digest(self, frames, offsets, lengths, mtu: int = 0, out=None, status=None, stream=None, op="digest",
+                       flags: int = FILL_CSUM):
         """A prepared digest_device call: the tensors are checked and the C arguments built ONCE,
-        and the returned callable enqueues the same fs_digest_batch (op "fcs": fs_digest_batch_fcs)
-        again on every call, with no per-call validation or marshalling. For a caller that digests
-        a fixed set of resident batches into fixed result slots over and over (a NIC ring's
-        buffers, the bench's rotated batches): the per-call host cost is the C call alone. The
-        callable keeps the tensors alive and raises FramesumError on a failed call."""
+        and the returned callable enqueues the same fs_digest_batch (op "fcs": fs_digest_batch_fcs;
+        op "fill": fs_fill_batch with `flags`) again on every call, with no per-call validation or
+        marshalling. For a caller that digests a fixed set of resident batches into fixed result
+        slots over and over (a NIC ring's buffers, the bench's rotated batches): the per-call host
+        cost is the C call alone. The callable keeps the tensors alive and raises FramesumError on
+        a failed call."""
         n, out, status, stream = self._device_args(frames, offsets, lengths, out, status, stream)
-        name = {"digest": "fs_digest_batch", "fcs": "fs_digest_batch_fcs"}[op]
+        name = {"digest": "fs_digest_batch", "fcs": "fs_digest_batch_fcs", "fill": "fs_fill_batch"}[op]
         fn = self.lib[name]  # a fresh function pointer with no argtypes: the ctypes objects go as built
         vp, u32 = ctypes.c_void_p, ctypes.c_uint32
-        args = (vp(self._ctx.value), vp(frames.data_ptr()), vp(offsets.data_ptr()), vp(lengths.data_ptr()), u32(n),
-                u32(mtu), vp(out.data_ptr()), vp(status.data_ptr()), vp(stream.cuda_stream))
+        mid = (u32(n), u32(mtu), u32(flags)) if op == "fill" else (u32(n), u32(mtu))
+        args = (vp(self._ctx.value), vp(frames.data_ptr()), vp(offsets.data_ptr()), vp(lengths.data_ptr()), *mid,
+                vp(out.data_ptr()), vp(status.data_ptr()), vp(stream.cuda_stream))
         keep = (frames, offsets, lengths, out, status, stream)
 
         def call():
