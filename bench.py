@@ -35,6 +35,12 @@ import time
 
 import numpy as np
 
+# Kernel arguments in device memory (read by the dispatch from HBM, not across PCIe from pinned
+# host memory): a HIP runtime setting read when the runtime initializes, so it is set before torch
+# loads it; a caller's own setting wins. The driver's command ran 4,604-4,686 GiB/s with it against
+# 4,466-4,598 without, interleaved on one box (profiles/round4/session2/env_sweep_driver_cmd.jsonl).
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 

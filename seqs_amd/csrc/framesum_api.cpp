@@ -566,8 +566,8 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
     ctx->err.clear();
-    if (variant != 0 && variant != 2 && variant != 4 && variant != 6)
-        return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0 (automatic), 2, 4 or 6");
+    if (variant != 0 && variant != 2 && variant != 4)
+        return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0 (automatic), 2 or 4");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
 }

@@ -32,15 +32,7 @@ struct FsTables {
     // T[b][1 << j] of the 40 plain [4][256] tables above, in LDS-image order (piece p = 4 t + b is the
     // 1-KB piece at LDS byte 1024 p): the kernels build them in place by VALU, as region A
     uint32_t plain_basis[40][8];
-    // The 16-lane kernel (digest_kernel_w): its row step is Z_256 (256-B rows), built in place into
-    // the first 128 B of each entry row of its region from this basis; and its 48 plain pieces
-    // (kW2Plain order: Z16 Z32 Z48 Z64 Z128 Z192 Z12 Z8 Z4 Z3 Z2 Z1, byte table b of operator t
-    // at piece 4 t + b), built in place from these bases.
-    uint32_t z256_basis[4][8];
-    uint32_t w2plain_basis[48][8];
 };
-// the byte shifts of the 16-lane kernel's 12 plain operators, in LDS order
-constexpr int kW2PlainShift[12] = {16, 32, 48, 64, 128, 192, 12, 8, 4, 3, 2, 1};
 constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 10;  // the LDS image: everything before z64_basis
 static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout");
 static_assert(offsetof(FsTables, z32) == 65536 && offsetof(FsTables, plain_basis) == kTablesLdsBytes + 128,

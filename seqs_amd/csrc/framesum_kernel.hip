@@ -1606,423 +1606,23 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 
 
 // =======================================================================================
-// The 16-lane kernel (digest_kernel_w, variant 6).
+// The 16-lane kernel (digest_kernel_w).
 //
-// The 4-lane kernels stream 16 frames per wave at once, 64 B each per load instruction; the
-// memory system reads that pattern ~11% slower than 4 frames per wave at 256 B each
-// (tools/tile_pattern.hip). This kernel streams a wave's 16 frames as 4 SUB-TILES of 4 frames:
-// sub-tile s is the quad (4 consecutive frames) gw + NW (4 j + s) of the wave's tile j, so the
-// chip's concurrent sub-tiles spread over the whole batch. In a sub-tile lane L streams frame
-// fj = L >> 4, 16-B chunk ch = L & 15 of every 256-B row; rows are anchored at the frame's
-// dword-rounded end (row r holds frame dwords nd - 64 (P - r) + [0, 64)), so an MTU frame is
-// exactly 6 rows and the sub-tile one block of the 6-row ring. The ring runs through the
-// sub-tiles and tiles: a sub-tile's last block refills it with the next sub-tile's first rows.
-// Each lane keeps 4 dword streams with A <- Z256(A) ^ w (region W: Z256, replicated as region A).
-// A sub-tile ends with the 64-stream combine of each frame in this layout (Z12/Z8/Z4 within a
-// lane, then Z_(16 (15 - ch)) as Z16a and Z64b, then a DPP reduction over the frame's 16 lanes),
-// parked per frame in LDS with the checksum partial. Everything else per frame runs once per
-// 16 frames in the 4-lane layout (group g = 4 s + f): the header slots are captured from the
-// sub-tiles' first rows, the parse runs after the last sub-tile's first rows (its loads in
-// flight), and the finish reads the parked combine.
-constexpr int kRingW = 6;
-constexpr uint32_t kW2Z16 = 0, kW2Z32 = 4096, kW2Z48 = 8192, kW2Z64 = 12288, kW2Z128 = 16384, kW2Z192 = 20480,
-                   kW2Z12 = 24576, kW2Z8 = 28672, kW2Zfin = 32768;  // Z4 Z3 Z2 Z1 (zfin[t] = Z_(4-t))
-constexpr uint32_t kW2Region = 49152;  // 64 KB: [entry][256 B], Z256's 4 byte tables x 8 copies in the first 128 B
-constexpr uint32_t kW2Cells = 9;       // slot cells: frame dwords [0, 33) at any slot offset xo <= 3
-constexpr uint32_t kW2HdrStride = kW2Cells * 256u;
-constexpr uint32_t kW2Hdr = kW2Region + 65536;
-constexpr uint32_t kW2Park = kW2Hdr + kWavesPerBlock * kW2HdrStride;  // per wave: 16 frames x {Y, csum}
-// per wave: the descriptors of two tiles (the current one and the next, alternating), written by
-// LDS-DMA as [field: S lo, S hi, len][group] dwords, so no VGPR holds them across the rows
-constexpr uint32_t kW2Desc = kW2Park + kWavesPerBlock * 128u;
-constexpr uint32_t kW2DescStride = 2u * 192u;
-constexpr uint32_t kW2LdsBytes = kW2Desc + kWavesPerBlock * kW2DescStride;
-static_assert(kW2LdsBytes <= kLdsBytes, "the 16-lane kernel's LDS map fits the shared array");
-static_assert(kW2Region < 65536, "region W's base folds into the ds_read offset field");
-static_assert(kW2Zfin + 16384 == kW2Region, "48 plain pieces before region W");
-
-// Region W and the 48 plain pieces in place by VALU from their bases (as build_region_a).
-__device__ __forceinline__ void build_tables_w2(const FsTables* __restrict__ tabs, char* lds) {
-    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-    const uint32_t t = threadIdx.x;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const uint32_t lane = t & 63u;
-    const uint64_t sz = sgpr_addr(&tabs->z256_basis[0][0]);
-    const uint64_t s0 = sgpr_addr(&tabs->w2plain_basis[w][0]);
-    const uint64_t s1 = sgpr_addr(&tabs->w2plain_basis[w + 16u][0]);
-    const uint64_t s2 = sgpr_addr(&tabs->w2plain_basis[w + 32u][0]);
-    u32x8 z0, z1, z2, z3, pb0, pb1, pb2;
-    asm volatile(
-        "s_load_dwordx8 %0, %7, 0x0\n\ts_load_dwordx8 %1, %7, 0x20\n\ts_load_dwordx8 %2, %7, 0x40\n\t"
-        "s_load_dwordx8 %3, %7, 0x60\n\ts_load_dwordx8 %4, %8, 0x0\n\ts_load_dwordx8 %5, %9, 0x0\n\t"
-        "s_load_dwordx8 %6, %10, 0x0\n\ts_waitcnt lgkmcnt(0)"
-        : "=&s"(z0), "=&s"(z1), "=&s"(z2), "=&s"(z3), "=&s"(pb0), "=&s"(pb1), "=&s"(pb2)
-        : "s"(sz), "s"(s0), "s"(s1), "s"(s2));
-    const uint32_t k = t & 7u, b = k >> 1, e = t >> 3;  // e < 128
-    uint32_t v = 0, top = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t lo = (b & 1u) ? z1[j] : z0[j];
-        const uint32_t hi = (b & 1u) ? z3[j] : z2[j];
-        const uint32_t bj = (b & 2u) ? hi : lo;
-        if (j < 7) v ^= bj & (0u - ((e >> j) & 1u));
-        else top = bj;
-    }
-    *reinterpret_cast<u32x4*>(lds + kW2Region + e * 256u + 16u * k) = u32x4{v, v, v, v};
-    v ^= top;
-    *reinterpret_cast<u32x4*>(lds + kW2Region + (e + 128u) * 256u + 16u * k) = u32x4{v, v, v, v};
-    auto piece = [&](const u32x8& pb, uint32_t p) {
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
-        const uint32_t x1 = x ^ pb[0];
-        *reinterpret_cast<u32x4*>(lds + 1024u * p + 16u * lane) = u32x4{x, x1, x ^ pb[1], x1 ^ pb[1]};
-    };
-    piece(pb0, w);
-    piece(pb1, w + 16u);
-    piece(pb2, w + 32u);
-}
-
-// Z_k(v) for any k from the 16-lane kernel's tables (TX fill): Z256 steps (region W, copy 0),
-// then Z192/Z128/Z64, Z48/Z32/Z16, Z12/Z8/Z4 and Z3/Z2/Z1.
-__device__ __forceinline__ uint32_t zshift_w2(const char* lds, uint32_t v, uint32_t k) {
-    for (; k >= 256u; k -= 256u)
-        v = lds32(lds, kW2Region + ((v & 0xffu) << 8)) ^ lds32(lds, kW2Region + (((v >> 8) & 0xffu) << 8) + 32u) ^
-            lds32(lds, kW2Region + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kW2Region + ((v >> 24) << 8) + 96u);
-    const uint32_t m = (k >> 6) & 3u, a = (k >> 4) & 3u, c = (k >> 2) & 3u, t = k & 3u;
-    if (m) v = zplain(lds, v, m == 1u ? kW2Z64 : m == 2u ? kW2Z128 : kW2Z192);
-    if (a) v = zplain(lds, v, a == 1u ? kW2Z16 : a == 2u ? kW2Z32 : kW2Z48);
-    if (c) v = zplain(lds, v, c == 1u ? kW2Zfin : c == 2u ? kW2Z8 : kW2Z12);
-    if (t) v = zplain(lds, v, kW2Zfin + 4096u * (4u - t));
-    return v;
-}
-struct LayoutW2 {
-    __device__ static __forceinline__ uint32_t shift(const char* lds, uint32_t v, uint32_t k) { return zshift_w2(lds, v, k); }
-    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
-        return zplain(lds, v, kW2Zfin + 4096u * t);
-    }
-    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) { return lds32(lds, kW2Zfin + 3u * 4096u + (i << 2)); }
-};
-
-// A row load the compiler does not track (inline asm) and its exact wait: every block refills
-// every ring slot (a dummy address when nothing is left), so when slot i is consumed the loads
-// issued after it are the other kRingW - 1 slots'.
-__device__ __forceinline__ u32x4 load_row_asm(const uint32_t* p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-template <int N>
-__device__ __forceinline__ void wait_row(u32x4& v) {
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "n"(N));
-}
-
-// A sub-tile in the 16-lane layout: the lane's frame (group 4 s + fj of the tile, from the LDS
-// descriptor table) and where its rows are.
-struct SubW {
-    const uint32_t* fb;  // frame dword 0 of the lane's loads (an empty lane: a longest frame's)
-    int x00;             // frame dword of this lane's chunk in row 0 (of the loads' frame)
-    int nd;              // own stream dwords (0: empty lane or a frame under 4 bytes)
-    int lo;              // lowest frame dword a clamped load may start at
-    uint32_t sat;        // S & 3 | tail mask bytes << 2 (te, 1..4)
-    int P;               // wave-uniform: rows (a multiple of kRingW; 0: nothing to stream)
-    int H;               // wave-uniform: leading rows that take the masked path
-    int Hc;              // wave-uniform: leading rows holding slot cells (frame dwords < 36)
-};
-
-// The 4 frames of a sub-tile sit in the wave's 4 rows of 16 lanes, one frame per row: a wave
-// max of a frame value is a max over 4 readlanes.
-__device__ __forceinline__ int rows_max(int x) {
-    return max(max(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
-               max(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
-}
-
-// sub-tile state from the descriptor table `dt` (LDS byte address) of a tile whose frame of group
-// g is valid when bit g of `vmask` is set (kOpsFcs: the rows stream the frame without its FCS)
-template <uint32_t kOps>
-__device__ __forceinline__ SubW sub_state(int s, uint32_t fj, uint32_t ch, uint32_t dt, uint32_t vmask,
-                                          const uint8_t* __restrict__ frames) {
-    SubW R;
-    const char* lds = g_lds;
-    const uint32_t g = 4u * (uint32_t)s + fj;
-    const uint32_t slo = lds32(lds, dt + 4u * g), shi = lds32(lds, dt + 64u + 4u * g);
-    uint32_t ln = ((vmask >> g) & 1u) ? lds32(lds, dt + 128u + 4u * g) : 0u;
-    if (kOps == kOpsFcs) ln = ln >= 4u ? ln - 4u : 0u;
-    const uint32_t sa = slo & 3u;
-    R.nd = ln >= 4u ? (int)((sa + ln + 3u) >> 2) : 0;
-    const int rows = (R.nd + 63) >> 6;
-    const int Rx = rows_max(rows);
-    R.P = (Rx + kRingW - 1) / kRingW * kRingW;
-    const uint32_t e = (sa + ln) & 3u;
-    R.sat = sa | ((e ? e : 4u) << 2);
-    uint64_t ld_sdw = (((uint64_t)shi << 32) | slo) >> 2;
-    int ld_nd = R.nd;
-    {   // an empty lane loads the chunks of a longest frame of the sub-tile (its own results are
-        // discarded), so that every row load stays inside a frame
-        const int srcl = (int)__builtin_ctzll(__ballot(rows == Rx));
-        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ld_sdw, srcl);
-        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ld_sdw >> 32), srcl);
-        const int s_nd = __builtin_amdgcn_readlane(R.nd, srcl);
-        if (R.nd == 0) {
-            ld_sdw = ((uint64_t)s_hi << 32) | s_lo;
-            ld_nd = s_nd;
-        }
-    }
-    R.fb = reinterpret_cast<const uint32_t*>(frames + (ld_sdw << 2));
-    R.x00 = ld_nd - 64 * R.P + 4 * (int)ch;
-    R.lo = max(ld_sdw > (1u << 24) ? -(1 << 24) : -(int)ld_sdw, min(0, ld_nd - 4));
-    // masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
-    // dword before the frame (chunk 0 holds the row's lowest dword)
-    const int need = 2 - (R.nd - 64 * R.P);
-    R.H = rows_max(R.nd > 0 && need > 0 ? min((need + 63) >> 6, R.P) : 0);
-    // slot cells: rows up to the one holding frame dword 35
-    const int need_c = 36 - (R.nd - 64 * R.P);
-    R.Hc = rows_max(R.nd > 0 ? min((need_c + 63) >> 6, R.P) : 0);
-    return R;
-}
-
-// A masked row (16-lane layout): the chunk realigned when its load was clamped, the dwords
-// before the frame zeroed, head/tail bytes masked, the CRC init applied; returns the chunk as it
-// lies in the frame (for the header slot).
-__device__ __forceinline__ u32x4 masked_row_w2(const char* lds, const LaneKeys& k, u32x4 u, int rel, int p, int nd,
-                                               uint32_t sat, uint32_t (&A)[4], uint32_t& cs) {
-    const uint32_t sa = sat & 3u, te = sat >> 2;
-    const uint32_t head_mask = 0xffffffffu << (8u * sa);
-    const uint32_t tail_mask = te == 4u ? 0xffffffffu : ((1u << (8u * te)) - 1u);
-    const int sh = p - rel;
-    uint32_t v[4];
-    v[0] = u.x;
-    v[1] = (sh == 0) ? u.y : u.x;
-    v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
-    v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int x = rel + j;
-        uint32_t d = (x >= 0) ? v[j] : 0u;
-        uint32_t c = 0u;
-        if (x == 0) { d &= head_mask; c = head_mask; }
-        if (x == 1) c = ~head_mask;
-        if (x == nd - 1) d &= tail_mask;
-        A[j] = zrep<kW2Region>(lds, A[j], k, d ^ c);
-        cs = sad16(d, cs);
-    }
-    return u32x4{v[0], v[1], v[2], v[3]};
-}
-
-// The lane index from mbcnt, opaque to the compiler: values derived from it are recomputed where
-// they are used instead of being hoisted into registers held by the whole kernel.
-__device__ __forceinline__ uint32_t lane_id_opaque() {
-    uint32_t ln;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-    return ln;
-}
-
-template <uint32_t kOps>
-__global__ void __launch_bounds__(kThreads, 1)
-digest_kernel_w(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
-                const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
-                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx,
-                uint32_t fpt) {
-    (void)report;
-    (void)fpt;
-    char* lds = g_lds;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // (lane-derived indices are recomputed where used: lane_id_opaque)
-    const uint32_t NW = gridDim.x * kWavesPerBlock;
-    const uint32_t gw = first_tile(wave);
-    const uint32_t nq = (n + 3u) / 4u;
-    const uint32_t hw = __builtin_amdgcn_readfirstlane(kW2Hdr + wave * kW2HdrStride);
-    const uint32_t pk = __builtin_amdgcn_readfirstlane(kW2Park + wave * 128u);
-    const uint32_t dsc = __builtin_amdgcn_readfirstlane(kW2Desc + wave * kW2DescStride);
-    LaneKeys keys;
-    {
-        const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
-        keys.cvec = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) keys.cvec |= (32u * j + 4u * c) << (8u * j);
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t b = (k + h) & 3u;
-            keys.sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
-        }
-    }
-    // tile j's frame of group g (4-lane layout): frame g % 4 of quad gw + NW (4 j + g / 4)
-    auto quad_of = [&](uint32_t j, uint32_t g) { return gw + NW * (4u * j + (g >> 2)); };
-    auto frame_of = [&](uint32_t j, uint32_t g) {
-        const uint32_t q = quad_of(j, g);
-        return q < nq ? 4u * q + (g & 3u) : n;  // n: no frame
-    };
-    auto tile_valid = [&](uint32_t j) { return quad_of(j, 0) < nq; };
-    // bit g: tile j's group g has a frame (wave-uniform)
-    auto valid_mask = [&](uint32_t j) {
-        uint32_t m = 0;
-        for (uint32_t g = 0; g < 16u; ++g) m |= (frame_of(j, g) < n ? 1u : 0u) << g;
-        return __builtin_amdgcn_readfirstlane(m);
-    };
-    // tile j's descriptors into table buffer b by LDS-DMA (lanes < 16: group = lane)
-    auto issue_desc = [&](uint32_t j, uint32_t b) {
-        const uint32_t lane = lane_id_opaque();
-        const uint32_t f = frame_of(j, lane & 15u);
-        const uint32_t fc = f < n ? f : n - 1u;
-        const uint32_t base = __builtin_amdgcn_readfirstlane(lds_base(lds) + dsc + 192u * b);
-        if (lane < 16u) {
-            dma_x1(reinterpret_cast<const uint32_t*>(offsets + fc), base);
-            dma_x1(reinterpret_cast<const uint32_t*>(offsets + fc) + 1, base + 64u);
-            dma_x1(lengths + fc, base + 128u);
-        }
-    };
-
-    const uint32_t* dummy = reinterpret_cast<const uint32_t*>(tabs);
-    u32x4 pf[kRingW];
-    SubW cur;
-    cur.P = 0;
-    const bool first = tile_valid(0);
-    if (first) issue_desc(0, 0);
-    build_tables_w2(tabs, lds);
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): tile 0's descriptor table (the only loads so far)
-    uint32_t vm = first ? valid_mask(0) : 0u;
-    if (first) {
-        const uint32_t l2 = lane_id_opaque();
-        cur = sub_state<kOps>(0, l2 >> 4, l2 & 15u, dsc, vm, frames);
-#pragma unroll
-        for (int i = 0; i < kRingW; ++i) {
-            const int x = cur.x00 + 64 * i;
-            pf[i] = load_row_asm(cur.P > 0 ? cur.fb + (i < cur.H ? load_pos(x, cur.lo) : x) : dummy);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < kRingW; ++i) pf[i] = load_row_asm(dummy);
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's table stores; the rows stay in flight
-    __builtin_amdgcn_s_barrier();
-    if ((wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // two-level age priority (as the one-pass kernel)
-
-    for (uint32_t j = 0; tile_valid(j); ++j) {
-        const uint32_t dt = dsc + 192u * (j & 1u);        // this tile's descriptor table
-        const uint32_t dtn = dsc + 192u * ((j + 1u) & 1u);  // the next tile's
-        const bool more = tile_valid(j + 1u);
-        uint32_t vmn = 0u;
-        for (int s = 0; s < 4; ++s) {
-            const uint32_t ln = lane_id_opaque();
-            const uint32_t fj = ln >> 4, ch = ln & 15u;
-            if (s == 2 && more) issue_desc(j + 1u, (j + 1u) & 1u);  // ahead of sub-tile 2's refills
-            // the refill target after this sub-tile: the next sub-tile, the next tile's first, or nothing
-            SubW nxt;
-            nxt.P = 0;
-            if (s < 3) {
-                nxt = sub_state<kOps>(s + 1, fj, ch, dt, vm, frames);
-            } else if (more) {
-                // the next tile's table: older than the ring's kRingW loads in flight
-                __builtin_amdgcn_s_waitcnt(0x0070 | kRingW);
-                vmn = valid_mask(j + 1u);
-                nxt = sub_state<kOps>(0, fj, ch, dtn, vmn, frames);
-            }
-            const bool tg = nxt.P > 0;
-            uint32_t A[4] = {0u, 0u, 0u, 0u};
-            uint32_t cs = 0u, junk = 0u;
-            const int Pc = cur.P / kRingW;
-            for (int c = 0; c < Pc; ++c) {
-                const bool lastc = c + 1 == Pc;
-                // this chunk's refills: chunk c + 1 of this sub-tile, or chunk 0 of the target
-                const uint32_t* tfb = lastc ? nxt.fb : cur.fb;
-                const int tx0 = lastc ? nxt.x00 : cur.x00 + 64 * kRingW * (c + 1);
-                const int tlo = lastc ? nxt.lo : cur.lo;
-                const int tH = lastc ? nxt.H : cur.H - kRingW * (c + 1);
-                const bool live = !lastc || tg;
-#pragma unroll
-                for (int i = 0; i < kRingW; ++i) {
-                    wait_row<kRingW - 1>(pf[i]);
-                    const u32x4 u = pf[i];
-                    const int r = kRingW * c + i;
-                    const int x0 = cur.x00 + 64 * r;
-                    u32x4 cell = u;
-                    if (r < cur.H) cell = masked_row_w2(lds, keys, u, x0, load_pos(x0, cur.lo), cur.nd, cur.sat, A, cs);
-                    else lean_row<kW2Region>(lds, keys, u, A, cs);
-                    if (r < cur.Hc) {  // header slot cells of group 4 s + fj
-                        const int xo = (-cur.nd) & 3;
-                        const int cc = (x0 + xo) >> 2;
-                        if (cur.nd > 0 && x0 + xo >= 0 && cc < (int)kW2Cells)
-                            *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)cc * 256u + (4u * (uint32_t)s + fj) * 16u) = cell;
-                    }
-                    if (lastc && i == kRingW - 1 && r >= cur.H && ch == 15u && cur.nd > 0) {
-                        const uint32_t te = cur.sat >> 2;
-                        junk = u.w & ~(te == 4u ? 0xffffffffu : ((1u << (8u * te)) - 1u));
-                    }
-                    const int xn = tx0 + 64 * i;
-                    pf[i] = load_row_asm(live ? tfb + (i < tH ? load_pos(xn, tlo) : xn) : dummy);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (s == 3 && c == (cur.Hc - 1) / kRingW) {
-                    // ---- header parse of the tile's 16 frames (4-lane layout), every slot captured
-                    const uint32_t l2 = lane_id_opaque();
-                    const uint32_t grp = l2 >> 2, gl = l2 & 3u;
-                    const uint32_t fi = frame_of(j, grp);
-                    const uint64_t S = ((uint64_t)lds32(lds, dt + 64u + 4u * grp) << 32) | lds32(lds, dt + 4u * grp);
-                    uint32_t len = fi < n ? lds32(lds, dt + 128u + 4u * grp) : 0u;
-                    if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
-                    const uint32_t sa4 = (uint32_t)S & 3u;
-                    const uint32_t nd4 = len >= 4u ? (sa4 + len + 3u) >> 2 : 0u;
-                    parse_tile<kOps, kHdrDwords>(hw, grp, gl, sa4, len, mtu,
-                                                 reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
-                                                 fi < n && gl == 0u, hw, (0u - nd4) & 3u);
-                }
-            }
-            if (s == 3 && cur.P == 0) {  // no rows in the last sub-tile: parse now
-                const uint32_t l2 = lane_id_opaque();
-                const uint32_t grp = l2 >> 2, gl = l2 & 3u;
-                const uint32_t fi = frame_of(j, grp);
-                const uint64_t S = ((uint64_t)lds32(lds, dt + 64u + 4u * grp) << 32) | lds32(lds, dt + 4u * grp);
-                uint32_t len = fi < n ? lds32(lds, dt + 128u + 4u * grp) : 0u;
-                if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
-                const uint32_t sa4 = (uint32_t)S & 3u;
-                const uint32_t nd4 = len >= 4u ? (sa4 + len + 3u) >> 2 : 0u;
-                parse_tile<kOps, kHdrDwords>(hw, grp, gl, sa4, len, mtu,
-                                             reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)),
-                                             fi < n && gl == 0u, hw, (0u - nd4) & 3u);
-            }
-            // ---- the sub-tile's combine (16-lane layout): the pending register of each frame's
-            // last dword, Y = xor over its 64 streams of Z_(4 (63 - p))(A_p), p = 4 ch + j
-            {
-                const uint32_t U = zplain(lds, A[0], kW2Z12) ^ zplain(lds, A[1], kW2Z8) ^
-                                   zplain(lds, A[2], kW2Zfin) ^ A[3] ^ junk;
-                const uint32_t sh = 15u - ch, a = sh & 3u, b = sh >> 2;
-                const uint32_t v1 = zplain(lds, U, a == 1u ? kW2Z16 : a == 2u ? kW2Z32 : kW2Z48);
-                const uint32_t V = a ? v1 : U;
-                const uint32_t v2 = zplain(lds, V, b == 1u ? kW2Z64 : b == 2u ? kW2Z128 : kW2Z192);
-                uint32_t Y = b ? v2 : V;
-                Y ^= dpp_quad<kQuadXor1>(Y);
-                Y ^= dpp_quad<kQuadXor2>(Y);
-                Y ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)Y, 0x124, 0xf, 0xf, false);  // row_ror:4
-                Y ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)Y, 0x128, 0xf, 0xf, false);  // row_ror:8
-                cs -= sad16(junk, 0u);
-                cs = (cs & 0xffffu) + (cs >> 16);
-                cs += dpp_quad<kQuadXor1>(cs);
-                cs += dpp_quad<kQuadXor2>(cs);
-                cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0x124, 0xf, 0xf, false);
-                cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0x128, 0xf, 0xf, false);
-                if (ch == 0u) *reinterpret_cast<uint2*>(lds + pk + 8u * (4u * (uint32_t)s + fj)) = make_uint2(Y, cs);
-            }
-            cur = nxt;
-        }
-        // ---- finish (4-lane layout): the group's lane 0
-        {
-            const uint32_t l2 = lane_id_opaque();
-            const uint32_t grp = l2 >> 2, gl = l2 & 3u;
-            const uint32_t fi = frame_of(j, grp);
-            if (fi < n && gl == 0u) {
-                const uint64_t S = ((uint64_t)lds32(lds, dt + 64u + 4u * grp) << 32) | lds32(lds, dt + 4u * grp);
-                uint32_t len = lds32(lds, dt + 128u + 4u * grp);
-                if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
-                const uint2 yc = *reinterpret_cast<const uint2*>(lds + pk + 8u * grp);
-                const uint32_t e = ((uint32_t)S + len) & 3u;
-                finish_frame<kOps, LayoutW2>(lds, unpark_parsed<kOps>(lds, hw, grp), S, len, e ? e : 4u, yc.x, yc.y,
-                                             frames, wframes, lengths, fi, out, status, tx);
-            }
-        }
-        vm = vmn;
-    }
-}
+// A wave owns a SUPER-TILE of 16 consecutive frames (8 or 4 for small batches). The header
+// DMA, the parse and the finish work on it as the 4-lane kernels do (4 lanes per frame). The
+// rows stream in PASSES of 4 frames with a GROUP of 16 lanes per frame: 256-byte rows
+// anchored at the frame's dword-rounded end, lane j of the group loading dwords [4j, 4j+4)
+// of every row (16 B/lane, a 256-B contiguous piece per frame per load instruction -- the
+// access pattern that reads at the plain-stream rate, tools/tile_pattern.hip). The frames are
+// ordered by row count into the passes, so a pass holds frames of similar length. Each lane
+// keeps 4 dword streams with A <- Z256(A) ^ w (region A holds Z_256); a pass ends with the
+// 64-stream combine of each frame (Z12/Z8/Z4 within a lane, Z48/Z32/Z16 within a quad of
+// lanes, Z192/Z128/Z64 across the quads), parked per frame in LDS for the finish.
+// One ring of kPfW row loads runs through the whole launch: a pass's last block refills the
+// ring with the next pass's (or the next super-tile's) first rows, so the loads never drain
+// between passes. The next super-tile's descriptors are loaded one super-tile ahead, its
+// geometry (ordering, rows per pass) and header DMA are set up at the current super-tile's
+// last block.
 
 }  // namespace
 
@@ -2075,7 +1675,6 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         }
     }
     if (force) mixed = force == 2;  // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
-    const bool wide = force == 6;   // 6: the 16-lane kernel (digest_kernel_w)
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {
         if (report_host) report_host[kReportChosen] = v;
@@ -2093,28 +1692,18 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH(K)                                                                                        \
     hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
-    chosen(wide ? 6u : mixed ? 2u : 4u);
-    if (wide) {
-        // a wave's tile is 4 quads (4-frame sub-tiles) strided by the grid's waves
-        const uint32_t quads = (n + 3u) / 4u;
-        uint32_t wb = (quads + kWavesPerBlock * 4u - 1u) / (kWavesPerBlock * 4u);
-        if (wb > max_blocks) wb = max_blocks;
-        blocks = wb;
-    }
+    chosen(mixed ? 2u : 4u);
     switch (op) {
     case FsOp::kDigest:
-        if (wide) FS_LAUNCH((digest_kernel_w<kOpsDigest>));
-        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
         else FS_LAUNCH((digest_kernel_a<kOpsDigest>));
         break;
     case FsOp::kFill:
-        if (wide) FS_LAUNCH((digest_kernel_w<kOpsTx>));
-        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
         else FS_LAUNCH((digest_kernel_a<kOpsTx>));
         break;
     case FsOp::kFcs:
-        if (wide) FS_LAUNCH((digest_kernel_w<kOpsFcs>));
-        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
+        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
         else FS_LAUNCH((digest_kernel_a<kOpsFcs>));
         break;
     }

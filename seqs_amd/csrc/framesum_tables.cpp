@@ -71,18 +71,6 @@ void build_tables(FsTables* t) {
                 if ((e >> j) & 1u) v ^= t->plain_basis[p][j];
             if (v != plain[256 * p + e]) throw std::logic_error("plain table basis mismatch");
         }
-    // the 16-lane kernel's row step and plain pieces (bases only: built in place on the device)
-    {
-        static uint32_t zt[4][256];
-        op_table(t1, 256, zt);
-        for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t j = 0; j < 8; ++j) t->z256_basis[b][j] = zt[b][1u << j];
-        for (int k = 0; k < 12; ++k) {
-            op_table(t1, kW2PlainShift[k], zt);
-            for (uint32_t b = 0; b < 4; ++b)
-                for (uint32_t j = 0; j < 8; ++j) t->w2plain_basis[4 * k + b][j] = zt[b][1u << j];
-        }
-    }
     // The final step Z_(4-t) replaces "Z_4 then undo t appended zero bytes"; Z_1[0] is the
     // standard byte table used for frames shorter than 4 bytes.
     if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");
