@@ -164,6 +164,9 @@ def parse():
                         "launches run first, over the streams, without the gather (reported as prewarm_launches)")
     p.add_argument("--kernel", type=int, default=0,
                    help="fs_ctx_set_kernel variant: 0 automatic, 2 mixed-length, 4 one-pass")
+    p.add_argument("--workgroups", type=int, default=0,
+                   help="fs_ctx_set_workgroups: workgroups per launch (0: one per CU; fewer give each wave several "
+                        "tiles and let consecutive launches run side by side)")
     p.add_argument("--region-clocks", default=None, metavar="PATH",
                    help="measurement aid: write the timed region's CLOCK_MONOTONIC / CLOCK_BOOTTIME stamps (t0, "
                         "each step's return, t1) to PATH as JSON, to line them up with a rocprofv3 trace "
@@ -339,6 +342,8 @@ def main():
     n = args.frames or 65536
     engine = GPU.engine(local)
     engine.set_kernel(args.kernel)
+    if args.workgroups:
+        engine.set_workgroups(args.workgroups)
     batches = []
     for b in range(max(1, args.batches)):
         buf, off, ln = make_batch(args.config, n, seed=1 + 1000 * rank + b)
@@ -833,6 +838,8 @@ def run_c4(args, world, rank, local, dev, frames):
 
     n_global = frames
     engine = GPU.engine(local)
+    if getattr(args, "workgroups", 0):
+        engine.set_workgroups(args.workgroups)
     n = shard_count(n_global, world, rank)
     m = (n_global + world - 1) // world
     sb = shard_slab_bytes(n_global, world)

@@ -235,6 +235,13 @@ fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
  * meets mixed tiles; uniform traffic then moves to the one-pass kernel (4). */
 int fs_ctx_last_kernel(const fs_ctx* ctx);
 
+/* Workgroups per launch of a context's kernels: 0 (the default) launches one 16-wave
+ * workgroup per compute unit, so a batch of 65,536 frames gives every wave one tile of 16
+ * frames; k > 0 caps the grid at k workgroups (at most one per CU), so each wave streams
+ * several tiles back to back and consecutive launches on other streams run side by side on
+ * the remaining CUs. A negative value is FS_E_INVALID. Results never depend on it. */
+fs_status fs_ctx_set_workgroups(fs_ctx* ctx, int workgroups);
+
 /* Pinned host memory helpers for fs_digest_batch_host callers. */
 fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out);
 fs_status fs_host_free(fs_ctx* ctx, void* p);

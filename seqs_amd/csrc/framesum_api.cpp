@@ -55,6 +55,7 @@ struct fs_ctx {
     volatile uint32_t* h_report = nullptr;
     uint32_t* d_report = nullptr;
     int force_kernel = 0;  // fs_ctx_set_kernel
+    int workgroups = 0;    // fs_ctx_set_workgroups (0: one per CU)
     uint32_t next_launch_id = 1;  // the context's launch sequence (launch_digest: report ids, sticky window)
     HostSlot slot[kHostSlots];
     hipStream_t copy_stream = nullptr, compute_stream = nullptr;
@@ -156,7 +157,8 @@ fs_status quiesce_host_streams(fs_ctx* ctx) {
 hipError_t launch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                   uint32_t mtu, fs_digest* out, uint8_t* status, hipStream_t stream, framesum::FsOp op,
                   uint8_t* wframes, uint32_t tx) {
-    return framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status, stream, ctx->num_cus,
+    const int wgs = ctx->workgroups > 0 && ctx->workgroups < ctx->num_cus ? ctx->workgroups : ctx->num_cus;
+    return framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status, stream, wgs,
                                    ctx->h_report, ctx->d_report, &ctx->next_launch_id, ctx->force_kernel, op, wframes,
                                    tx);
 }
@@ -560,6 +562,14 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
     if (!gathered || !out || nshards == 0) return set_err(ctx, FS_E_INVALID, "fs_deinterleave: null pointer or no shards");
     FS_HIP(ctx, hipSetDevice(ctx->device));
     FS_HIP(ctx, framesum::launch_deinterleave(gathered, nshards, n, out, status, reinterpret_cast<hipStream_t>(stream)));
+    return FS_SUCCESS;
+}
+
+fs_status fs_ctx_set_workgroups(fs_ctx* ctx, int workgroups) {
+    if (!ctx) return FS_E_INVALID;
+    ctx->err.clear();
+    if (workgroups < 0) return set_err(ctx, FS_E_INVALID, "fs_ctx_set_workgroups: workgroups must be >= 0");
+    ctx->workgroups = workgroups;
     return FS_SUCCESS;
 }
 

@@ -67,6 +67,7 @@ EXPORTED_SYMBOLS = (
     "fs_digest_batch_fcs",
     "fs_digest_batch_multi",
     "fs_ctx_set_kernel",
+    "fs_ctx_set_workgroups",
     "fs_ctx_last_kernel",
     "fs_host_alloc",
     "fs_host_free",
@@ -134,6 +135,9 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.fs_digest_batch_fcs.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp]
     lib.fs_digest_batch_fcs.restype = ctypes.c_int32
     lib.fs_ctx_set_kernel.argtypes = [vp, ctypes.c_int]
+    if hasattr(lib, "fs_ctx_set_workgroups"):  # (absent from builds before round 4: same-box A/B runs)
+        lib.fs_ctx_set_workgroups.restype = i32
+        lib.fs_ctx_set_workgroups.argtypes = [vp, ctypes.c_int]
     lib.fs_ctx_last_kernel.argtypes = [vp]
     lib.fs_ctx_last_kernel.restype = ctypes.c_int
     lib.fs_digest_batch_multi.restype = i32
@@ -222,6 +226,11 @@ class Engine:
         of mixed-length tiles into pieces; 4 (KERNEL_ONE_PASS): the one-pass kernel (block-aligned
         rows). Any other value raises."""
         self._check(self.lib.fs_ctx_set_kernel(self._ctx, int(variant)), "fs_ctx_set_kernel")
+
+    def set_workgroups(self, workgroups: int) -> None:
+        """fs_ctx_set_workgroups: 0 (default) one 16-wave workgroup per CU; k > 0 at most k
+        workgroups per launch, each wave then streams several tiles back to back."""
+        self._check(self.lib.fs_ctx_set_workgroups(self._ctx, int(workgroups)), "fs_ctx_set_workgroups")
 
     def last_kernel(self) -> int:
         """The variant (2 or 4) this context's latest launch ran (0 before its first launch). With

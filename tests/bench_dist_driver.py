@@ -39,6 +39,9 @@ class FakeEngine:
     def set_kernel(self, v):
         pass
 
+    def set_workgroups(self, k):
+        pass
+
     def last_kernel(self):
         return 4
 

@@ -327,6 +327,56 @@ def test_many_tiles_per_wave(engine, n, flen):
     check(engine, buf, off, ln, label=f"many tiles n={n} len={flen}")
 
 
+def _tile_mix_batch(ntiles: int, seed: int):
+    """Tiles of 16 frames, each tile one random length class, so a wave streaming several tiles
+    meets every transition of the one-pass kernel's pipelined tile loop: tiles of frames under 4
+    bytes (no rows), one-block tiles (<= 5 blocks), two-block tiles, MTU and jumbo tiles, tiles of
+    widely mixed lengths (header slots loaded, not captured) and a partial last tile."""
+    rng = np.random.default_rng(seed)
+    classes = [(0, 3), (20, 300), (301, 620), (1400, 1514), (8000, 9000), (0, 3000)]
+    lens = []
+    for _ in range(ntiles):
+        lo, hi = classes[rng.integers(0, len(classes))]
+        lens.extend(rng.integers(lo, hi + 1, 16).tolist())
+    lens = lens[: 16 * ntiles - 5]
+    import random
+
+    import framegen
+    r = random.Random(seed)
+    frames = [framegen.valid_frame(r, 6 if i % 2 else 17, payload=max(0, L - 54))[:L] for i, L in enumerate(lens)]
+    return pack_frames(frames, align=1)
+
+
+@pytest.mark.parametrize("workgroups", [1, 7, 64])
+def test_few_workgroups(engine, workgroups):
+    """fs_ctx_set_workgroups: a capped grid gives each wave many tiles, streamed back to back (the
+    next tile's descriptors and first rows are in flight during the current tile's last block)."""
+    engine.set_workgroups(workgroups)
+    try:
+        buf, off, ln = synth.uniform_batch(20000, 1500, seed=workgroups)
+        check(engine, buf, off, ln, label=f"uniform wg={workgroups}")
+        buf, off, ln = _tile_mix_batch(600, seed=workgroups)
+        check(engine, buf, off, ln, label=f"tile mix wg={workgroups}")
+        check(engine, buf, off, ln, mtu=1514, label=f"tile mix mtu wg={workgroups}")
+    finally:
+        engine.set_workgroups(0)
+
+
+def test_set_workgroups_rejects_negative():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from seqs_amd import FramesumError
+
+    e = Engine(0)
+    try:
+        e.set_workgroups(0)
+        e.set_workgroups(3)
+        with pytest.raises(FramesumError, match="workgroups"):
+            e.set_workgroups(-1)
+    finally:
+        e.close()
+
+
 def test_auto_choice_first_launches():
     """Variant 0 (automatic): a fresh context's first launches run the mixed-length kernel, so a
     mixed batch is fast from its first call (the one-pass kernel's report would reach the host

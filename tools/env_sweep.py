@@ -22,6 +22,15 @@ SETTINGS = [
     ("streams=3", {}, ["--streams", "3"]),
     ("streams=4", {}, ["--streams", "4"]),
     ("streams=8", {}, ["--streams", "8"]),
+    ("wg=192", {}, ["--workgroups", "192"]),
+    ("wg=128", {}, ["--workgroups", "128"]),
+    ("wg=64", {}, ["--workgroups", "64"]),
+    ("wg=128,streams=8", {}, ["--workgroups", "128", "--streams", "8"]),
+    # a previous build of the library (seqs_amd/lib/ab/, built from an earlier commit's sources) for
+    # same-box A/B
+    ("lib=old", {"FRAMESUM_LIB": os.path.join(ROOT, "seqs_amd", "lib", "ab", "libframesum_old.so")}, []),
+    ("wg=32", {}, ["--workgroups", "32"]),
+    ("wg=16", {}, ["--workgroups", "16"]),
 ]
 
 
@@ -30,10 +39,11 @@ def main() -> None:
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--only", default=None, help="comma-separated setting names")
+    p.add_argument("--only", default=None, help="setting names separated by '+'")
+    p.add_argument("--extra", default="", help="more bench arguments for every run (space-separated)")
     p.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "env_sweep.jsonl"))
     a = p.parse_args()
-    sets = [s for s in SETTINGS if a.only is None or s[0] in a.only.split(",")]
+    sets = [s for s in SETTINGS if a.only is None or s[0] in a.only.split("+")]
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     res = {s[0]: [] for s in sets}
     with open(a.out, "a") as f:
@@ -42,7 +52,7 @@ def main() -> None:
                 e = dict(os.environ)
                 e.update(env)
                 cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(a.steps), "--warmup", str(a.warmup),
-                       "--cpu-seconds", "0", "--no-sub"] + extra
+                       "--cpu-seconds", "0", "--no-sub"] + extra + a.extra.split()
                 cp = subprocess.run(cmd, env=e, capture_output=True, text=True, timeout=180)
                 if cp.returncode != 0:
                     print(f"{name}: rc {cp.returncode}\n{cp.stderr[-2000:]}", flush=True)

@@ -46,10 +46,23 @@ def main():
         t0, t1 = r["t0"][ck], r["t1"][ck]
         kin = [(s, e) for s, e, n in ks if "digest" in n and t0 <= s <= t1]
         lin = [(s, e, f) for s, e, f in api if t0 <= s <= t1 and "aunch" in f]
+        us = lambda x: x / 1e3  # noqa: E731
+        if kin and not lin and r.get("steps"):
+            # kernel trace only (no HIP-API trace, whose own overhead inflates the host side): the
+            # first step's return stands for the first launch call's end
+            settled = r.get("settled", 0) + off[i]
+            s0 = r["steps"][0] + off[i]
+            steps = [x + off[i] for x in r["steps"]]
+            gaps = [us(b - a) for a, b in zip(steps, steps[1:])]
+            print(f"region {i}: wall {r['elapsed_us']:.1f} us | t0->1st step returned {us(s0 - t0):.1f} | "
+                  f"returned->1st kernel {us(kin[0][0] - s0):.1f} | t0->1st kernel {us(kin[0][0] - t0):.1f} | "
+                  f"kernel span {us(max(e for _, e in kin) - kin[0][0]):.1f} ({len(kin)} kernels, first "
+                  f"{us(kin[0][1] - kin[0][0]):.1f}) | last end->settled {us(settled - max(e for _, e in kin)):.1f} | "
+                  f"settled->t1 {us(t1 - settled):.1f} | step returns every {sum(gaps) / max(1, len(gaps)):.1f} us")
+            continue
         if not kin or not lin:
             print(f"region {i}: no kernels/launches inside")
             continue
-        us = lambda x: x / 1e3  # noqa: E731
         first_call = lin[0]
         settled = r.get("settled", 0) + off[i]
         steps = [x + off[i] for x in r.get("steps", [])]
