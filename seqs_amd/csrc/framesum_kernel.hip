@@ -1196,9 +1196,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     // Preamble: the first tile's descriptors (the first memory ops, one round trip) while the
     // tables are built in place by VALU; geometry; the first rows; the masked-row count and the
     // capture flag; one barrier once this wave's table stores are done.
-    // (readfirstlane: the wave index comes from threadIdx.x, so hipcc would treat the tile loop and
-    // every branch on the tile as divergent -- exec-masked, with vmcnt(0) at the joins)
-    uint32_t tile = __builtin_amdgcn_readfirstlane(gwave);
+    // (not readfirstlane'd: the wave-uniform form took 128 VGPRs against 118 and measured ~1% slower
+    // on C2, profiles/round4/session2/ab_pipelined_variants.jsonl)
+    uint32_t tile = gwave;
     FS_RTSTAMP(5);
     FS_STAMP(0);
     TileA T;

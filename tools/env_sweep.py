@@ -44,6 +44,10 @@ def main() -> None:
     p.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "env_sweep.jsonl"))
     a = p.parse_args()
     sets = [s for s in SETTINGS if a.only is None or s[0] in a.only.split("+")]
+    # lib=<name> not listed above: seqs_amd/lib/ab/libframesum_<name>.so (an A/B build)
+    for nm in (a.only or "").split("+"):
+        if nm.startswith("lib=") and nm not in [x[0] for x in sets]:
+            sets.append((nm, {"FRAMESUM_LIB": os.path.join(ROOT, "seqs_amd", "lib", "ab", f"libframesum_{nm[4:]}.so")}, []))
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     res = {s[0]: [] for s in sets}
     with open(a.out, "a") as f:
