@@ -163,7 +163,7 @@ def parse():
                    help="device pre-warm: when --warmup is below this, (min-warm - warmup) extra untimed "
                         "launches run first, over the streams, without the gather (reported as prewarm_launches)")
     p.add_argument("--kernel", type=int, default=0,
-                   help="fs_ctx_set_kernel variant: 0 automatic, 2 mixed-length, 4 one-pass")
+                   help="fs_ctx_set_kernel variant: 0 automatic, 2 mixed-length, 4 one-pass, 8 small-frame")
     p.add_argument("--workgroups", type=int, default=0,
                    help="fs_ctx_set_workgroups: workgroups per launch (0: one per CU; fewer give each wave several "
                         "tiles and let consecutive launches run side by side)")
@@ -599,7 +599,7 @@ def main():
                 if traffic is not None else None,
                 "kernel": {0: "automatic: digest_kernel_a (one-pass) for uniform batches, digest_kernel_ab for mixed",
                            2: "digest_kernel_ab (mixed-length)", 4: "digest_kernel_a (one-pass)"}.get(args.kernel),
-                "kernel_chosen": {2: "digest_kernel_ab", 4: "digest_kernel_a"}.get(engine_last_kernel),
+                "kernel_chosen": {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine_last_kernel),
                 "kernel_avg_us": round(k_avg_ms * 1e3, 3),
                 "kernel_timing": "HIP events around K back-to-back launches on the launch stream",
                 "algorithmic_bytes_per_launch": bytes_per_batch,
@@ -699,7 +699,7 @@ def sub_record_c3(args, dev):
         batches.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)))
     nbytes = int(batches[0][2].sum().item())
     elapsed, k_ms = single_gpu_region(engine, batches, args.steps, args.warmup, args.min_warm, max(1, args.streams), dev)
-    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a"}.get(engine.last_kernel())
+    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine.last_kernel())
     engine.close()
     del batches
     return {

@@ -225,11 +225,14 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
  * hold it), and one that splits long frames into 768-byte pieces when a tile of 16
  * frames mixes very different lengths. By default (variant 0) every launch reports
  * whether its batch had such tiles and the next launch picks accordingly. 2 forces
- * the mixed-length kernel, 4 the one-pass kernel; any other value is FS_E_INVALID.
- * Results are identical in every case; only the speed differs. */
+ * the mixed-length kernel, 4 the one-pass kernel, 8 the small-frame kernel (one lane per
+ * frame, small workgroups: for traffic of short frames such as the reference's 47-byte
+ * benchmark frames; fs_digest_batch* and fs_digest_batch_fcs run it, a TX fill runs the
+ * automatic choice; frames longer than ~130 bytes stay correct but are slow there); any
+ * other value is FS_E_INVALID. Results are identical in every case; only the speed differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
-/* The variant (2 or 4, as above) the context's latest launch ran; 0 before its first
+/* The variant (2, 4 or 8, as above) the context's latest launch ran; 0 before its first
  * launch, FS_E_INVALID for a null context. With variant 0 a context's first 16
  * launches run the mixed-length kernel (2), which keeps itself chosen while it
  * meets mixed tiles; uniform traffic then moves to the one-pass kernel (4). */

@@ -576,8 +576,8 @@ fs_status fs_ctx_set_workgroups(fs_ctx* ctx, int workgroups) {
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
     ctx->err.clear();
-    if (variant != 0 && variant != 2 && variant != 4)
-        return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0 (automatic), 2 or 4");
+    if (variant != 0 && variant != 2 && variant != 4 && variant != 8)
+        return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0 (automatic), 2, 4 or 8");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
 }

@@ -1673,23 +1673,166 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 
 
 // =======================================================================================
-// The 16-lane kernel (digest_kernel_w).
-//
-// A wave owns a SUPER-TILE of 16 consecutive frames (8 or 4 for small batches). The header
-// DMA, the parse and the finish work on it as the 4-lane kernels do (4 lanes per frame). The
-// rows stream in PASSES of 4 frames with a GROUP of 16 lanes per frame: 256-byte rows
-// anchored at the frame's dword-rounded end, lane j of the group loading dwords [4j, 4j+4)
-// of every row (16 B/lane, a 256-B contiguous piece per frame per load instruction -- the
-// access pattern that reads at the plain-stream rate, tools/tile_pattern.hip). The frames are
-// ordered by row count into the passes, so a pass holds frames of similar length. Each lane
-// keeps 4 dword streams with A <- Z256(A) ^ w (region A holds Z_256); a pass ends with the
-// 64-stream combine of each frame (Z12/Z8/Z4 within a lane, Z48/Z32/Z16 within a quad of
-// lanes, Z192/Z128/Z64 across the quads), parked per frame in LDS for the finish.
-// One ring of kPfW row loads runs through the whole launch: a pass's last block refills the
-// ring with the next pass's (or the next super-tile's) first rows, so the loads never drain
-// between passes. The next super-tile's descriptors are loaded one super-tile ahead, its
-// geometry (ordering, rows per pass) and header DMA are set up at the current super-tile's
-// last block.
+// The small-frame kernel (digest_kernel_s, variant 8): ONE LANE PER FRAME,
+// 64 frames per wave, for batches of short frames (the reference's own benchmark sends 47-byte
+// UDP frames, stacks/benchmark_test.go:12-46). The 4-lane kernels spend a 104-KB table image,
+// a workgroup barrier and one 16-wave workgroup per CU on every launch; on 47-byte frames that
+// fixed cost is the whole launch. Here a workgroup is 4 waves with 52 KB of LDS (the Z_4..Z_1
+// tables, 16 KB, built in place from their bases, and the header slots), so three fit a CU and
+// consecutive launches overlap. Per lane: the frame's descriptor, its 16-B aligned chunks
+// (whole chunks never leave the pages that hold frame bytes) into the lane's header slot, then
+// the CRC as a Horner chain P <- Z4(P) ^ d over the frame's dwords read back from the slot (the
+// CRC init XOR-ed into frame bytes 0..3, as the 4-lane kernels do), the one's-complement sum,
+// the RecvEth parse and the finish of the 4-lane kernels (parse_frame, finish_frame).
+// Frames longer than the slot (~130 B) stay correct -- their dwords past the slot come from
+// global memory -- but slow: the variant is for short-frame traffic (fs_ctx_set_kernel).
+constexpr int kSmallWaves = 4;
+constexpr int kSmallSlotRows = 9;  // 36 dwords per frame: frame dwords [0, 33) at any chunk phase
+constexpr uint32_t kSmallQuad = kSmallSlotRows * 256u;  // 16 frames' slots ([x >> 2][frame][x & 3])
+constexpr uint32_t kSmallWave = 4u * kSmallQuad;
+constexpr uint32_t kSmallTables = 16384u;  // zfin: Z_4, Z_3, Z_2, Z_1 ([4][256] each)
+constexpr uint32_t kSmallLdsBytes = kSmallTables + kSmallWaves * kSmallWave;
+static_assert(kSmallLdsBytes <= 53248, "three small-kernel workgroups fit a CU's LDS");
+__shared__ __attribute__((aligned(16))) char s_lds[kSmallLdsBytes];
+
+struct LayoutS {
+    __device__ static __forceinline__ uint32_t fin(const char* lds, uint32_t v, uint32_t t) {
+        return zplain(lds, v, 4096u * t);
+    }
+    __device__ static __forceinline__ uint32_t byte1(const char* lds, uint32_t i) { return lds32(lds, 3u * 4096u + (i << 2)); }
+    __device__ static __forceinline__ uint32_t shift(const char*, uint32_t v, uint32_t) { return v; }  // (no TX op)
+};
+
+// sum of frame bytes [p0, p1) from the lane's slot (chunk phase xo), in the 16-bit-half domain
+__device__ __forceinline__ uint32_t lane_slot_sum(const char* lds, uint32_t hw, uint32_t g, uint32_t sa, uint32_t xo,
+                                                  int p0, int p1) {
+    uint32_t s = 0;
+    if (p1 <= p0) return s;
+    const int a0 = (int)sa + p0, a1 = (int)sa + p1;
+    for (int k = a0 >> 2; k <= (a1 - 1) >> 2; ++k) s = sad16(hdr_dw(lds, hw, g, xo + (uint32_t)k) & range_mask(k, a0, a1), s);
+    return s;
+}
+
+template <uint32_t kOps>
+__global__ void __launch_bounds__(kWave * kSmallWaves)
+digest_kernel_s(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+                const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
+                uint2* __restrict__ out, uint8_t* __restrict__ status) {
+    static_assert(kOps != kOpsTx, "the small-frame kernel has no TX fill");
+    char* lds = s_lds;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t g = lane & 15u;
+    const uint32_t hw = kSmallTables + wave * kSmallWave + (lane >> 4) * kSmallQuad;  // this lane's slot set
+    const uint32_t nwaves = gridDim.x * kSmallWaves;
+    const uint32_t ntiles = (n + 63u) / 64u;
+    uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * kSmallWaves + wave);
+
+    // the first tile's descriptors, then the tables while they fly
+    auto desc = [&](uint32_t t, uint64_t& S, uint32_t& len) {
+        const uint32_t fi = t * 64u + lane;
+        const uint32_t fc = fi < n ? fi : n - 1u;
+        S = offsets[fc];
+        len = fi < n ? lengths[fc] : 0u;
+    };
+    uint64_t S = 0;
+    uint32_t len = 0;
+    if (tile < ntiles) desc(tile, S, len);
+    {   // Z_4, Z_3, Z_2, Z_1 (plain pieces 8..23 of the 4-lane layout) in place: wave w builds
+        // pieces 8 + w + 4k, lane l the entries 4l .. 4l + 3 of each
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t p = 8u + wave + 4u * k;
+            const uint32_t* pb = tabs->plain_basis[p];
+            uint32_t x = 0;
+#pragma unroll
+            for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
+            const uint32_t x1 = x ^ pb[0];
+            *reinterpret_cast<u32x4*>(lds + 1024u * (p - 8u) + 16u * lane) = u32x4{x, x1, x ^ pb[1], x1 ^ pb[1]};
+        }
+    }
+    __syncthreads();
+
+    for (; tile < ntiles; tile += nwaves) {
+        const uint32_t fi = tile * 64u + lane;
+        const bool valid = fi < n;
+        if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
+        const uint32_t sa = (uint32_t)S & 3u;
+        const uint32_t xo = (uint32_t)(S >> 2) & 3u;  // frame dword 0's place in its 16-B chunk
+        const uint32_t nd = (sa + len + 3u) >> 2;     // dwords holding frame bytes
+        const uint32_t nch = valid && len > 0u ? (xo + nd + 3u) >> 2 : 0u;
+        const u32x4* cb = reinterpret_cast<const u32x4*>(frames + ((S >> 4) << 4));
+        // the frame's chunks into the slot (the chunks past the slot come from memory below)
+        u32x4 v[kSmallSlotRows];
+#pragma unroll
+        for (int c = 0; c < kSmallSlotRows; ++c)
+            if ((uint32_t)c < nch) v[c] = cb[c];
+#pragma unroll
+        for (int c = 0; c < kSmallSlotRows; ++c)
+            if ((uint32_t)c < nch) *reinterpret_cast<u32x4*>(lds + hw + (uint32_t)c * 256u + g * 16u) = v[c];
+        // the next tile's descriptors, behind this tile's chunks
+        uint64_t Sn = 0;
+        uint32_t lenn = 0;
+        if (tile + nwaves < ntiles) desc(tile + nwaves, Sn, lenn);
+
+        // CRC (pending-register Horner, zero init; the init XOR-ed into frame bytes 0..3) and the
+        // one's-complement sum over the frame's dwords [0, nd) (head and tail bytes masked)
+        const uint32_t head = 0xffffffffu << (8u * sa);
+        const uint32_t te = ((sa + len) & 3u) ? ((sa + len) & 3u) : 4u;
+        const uint32_t tailm = te == 4u ? 0xffffffffu : ((1u << (8u * te)) - 1u);
+        const uint32_t* fb = reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2));
+        uint32_t P = 0u, cs = 0u;
+        const uint32_t lim = valid && len >= 4u ? nd : 0u;
+        const uint32_t lim1 = min(lim, 4u * kSmallSlotRows - xo);  // the dwords in the slot
+        for (uint32_t x = 0; x < lim1; ++x) {
+            uint32_t d = hdr_dw(lds, hw, g, xo + x);
+            if (x == 0u) d &= head;
+            if (x + 1u == nd) d &= tailm;
+            cs = sad16(d, cs);
+            const uint32_t c = x == 0u ? head : x == 1u ? ~head : 0u;
+            P = zplain(lds, P, 0u) ^ d ^ c;  // Z_4 (zfin[0]) of the pending register
+        }
+        // a frame longer than the slot: its remaining 16-B chunks from memory, 4 in flight (correct
+        // for any length, but one lane streams the frame: the variant is for short frames)
+        for (uint32_t c = kSmallSlotRows; c < (lim ? nch : 0u); c += 4u) {
+            u32x4 u[4];
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i)
+                if (c + i < nch) u[i] = cb[c + i];
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) {
+#pragma unroll
+                for (uint32_t k = 0; k < 4u; ++k) {
+                    const uint32_t x = 4u * (c + i) + k - xo;
+                    if (c + i < nch && x < nd) {
+                        uint32_t d = u[i][k];
+                        if (x + 1u == nd) d &= tailm;
+                        cs = sad16(d, cs);
+                        P = zplain(lds, P, 0u) ^ d;
+                    }
+                }
+            }
+        }
+
+        // header parse (RecvEth's gates and the checksum corrections) from the slot, and the finish
+        if (valid) {
+            uint32_t hsum = 0;
+            int64_t pad = -1;
+            if (len >= 34u) {
+                const uint32_t d3 = __builtin_bswap32(frame_dw(lds, hw, g, sa, 3, xo));
+                const uint32_t off = 14u + ((d3 >> 8) & 0xfu) * 4u;
+                const uint32_t tl = __builtin_bswap32(frame_dw(lds, hw, g, sa, 4, xo)) >> 16;
+                const uint32_t end = (14u + tl) & 0xffffu;
+                hsum = lane_slot_sum(lds, hw, g, sa, xo, 0, (int)min(off, len));
+                if (end < len && xo + nd <= 4u * kSmallSlotRows) pad = (int64_t)lane_slot_sum(lds, hw, g, sa, xo, (int)end, (int)len);
+            }
+            const Parsed Pr = parse_frame<kOps, 32>(lds, hw, g, sa, len, mtu, hsum, pad, fb, xo);
+            finish_frame<kOps, LayoutS>(lds, Pr, S, len, te, P, cs, frames, nullptr, lengths, fi, out, status, 0u);
+        }
+        S = Sn;
+        len = lenn;
+    }
+}
 
 }  // namespace
 
@@ -1742,6 +1885,9 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         }
     }
     if (force) mixed = force == 2;  // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
+    // 8: the small-frame kernel (RX digest and FCS verify; a TX fill runs the automatic choice)
+    const bool small = force == 8 && op != FsOp::kFill;
+    if (force == 8) mixed = false;
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {
         if (report_host) report_host[kReportChosen] = v;
@@ -1759,7 +1905,19 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH(K)                                                                                        \
     hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
-    chosen(mixed ? 2u : 4u);
+    chosen(small ? 8u : mixed ? 2u : 4u);
+    if (small) {
+        const uint32_t stiles = (n + 63u) / 64u;  // 64 frames (one per lane) per wave
+        uint32_t sb = (stiles + kSmallWaves - 1u) / kSmallWaves;
+        if (sb > 2u * max_blocks) sb = 2u * max_blocks;
+        if (op == FsOp::kFcs)
+            hipLaunchKernelGGL((digest_kernel_s<kOpsFcs>), dim3(sb), dim3(kWave * kSmallWaves), 0, stream, frames,
+                               offsets, lengths, n, mtu, tables, reinterpret_cast<uint2*>(out), status);
+        else
+            hipLaunchKernelGGL((digest_kernel_s<kOpsDigest>), dim3(sb), dim3(kWave * kSmallWaves), 0, stream, frames,
+                               offsets, lengths, n, mtu, tables, reinterpret_cast<uint2*>(out), status);
+        return hipGetLastError();
+    }
     switch (op) {
     case FsOp::kDigest:
         if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));

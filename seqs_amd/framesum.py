@@ -218,13 +218,15 @@ class Engine:
             raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
 
     # kernel variants (fs_ctx_set_kernel): results are identical, only the speed differs
-    KERNEL_AUTO, KERNEL_MIXED, KERNEL_ONE_PASS = 0, 2, 4
+    KERNEL_AUTO, KERNEL_MIXED, KERNEL_ONE_PASS, KERNEL_SMALL = 0, 2, 4, 8
 
     def set_kernel(self, variant: int) -> None:
         """0 (KERNEL_AUTO): automatic (the mixed-length kernel after a batch that had mixed-length
         tiles, the one-pass kernel otherwise); 2 (KERNEL_MIXED): the kernel that splits long frames
         of mixed-length tiles into pieces; 4 (KERNEL_ONE_PASS): the one-pass kernel (block-aligned
-        rows). Any other value raises."""
+        rows); 8 (KERNEL_SMALL): one lane per frame, for short-frame traffic (RX digest and FCS
+        verify; a TX fill then runs the automatic choice; long frames stay correct but slow). Any
+        other value raises."""
         self._check(self.lib.fs_ctx_set_kernel(self._ctx, int(variant)), "fs_ctx_set_kernel")
 
     def set_workgroups(self, workgroups: int) -> None:

@@ -57,7 +57,7 @@ def _batch(phase: int, room: int):
     return _CACHE[key]
 
 
-@pytest.fixture(scope="module", params=[4, 2, 0], ids=["one_pass", "mixed", "auto"])
+@pytest.fixture(scope="module", params=[4, 2, 0, 8], ids=["one_pass", "mixed", "auto", "small"])
 def engine(request):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

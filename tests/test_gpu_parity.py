@@ -21,8 +21,8 @@ from seqs_amd import Engine, pack_frames, split_digests, synth  # noqa: E402
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_AUTO],
-                ids=["one_pass", "mixed", "auto"])
+@pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_AUTO,
+                                        Engine.KERNEL_SMALL], ids=["one_pass", "mixed", "auto", "small"])
 def engine(request):
     # every case through every kernel variant (and the automatic choice)
     if not torch.cuda.is_available():
@@ -412,17 +412,17 @@ def test_auto_choice_first_launches():
 
 
 def test_set_kernel_accepts_shipped_variants_only():
-    """fs_ctx_set_kernel: 0 (automatic), 2 (mixed-length) and 4 (one-pass) only (VERDICT round 2,
-    item 6: the losing variants were removed from the library)."""
+    """fs_ctx_set_kernel: 0 (automatic), 2 (mixed-length), 4 (one-pass) and 8 (small-frame) only
+    (the losing variants were removed from the library)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from seqs_amd import FramesumError
 
     e = Engine(0)
     try:
-        for v in (0, 2, 4):
+        for v in (0, 2, 4, 8):
             e.set_kernel(v)
-        for v in (-1, 1, 3, 5, 6, 7):
+        for v in (-1, 1, 3, 5, 6, 7, 9):
             with pytest.raises(FramesumError, match="variant"):
                 e.set_kernel(v)
     finally:

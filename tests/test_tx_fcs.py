@@ -105,7 +105,7 @@ def _dev(x, torch):
     return torch.from_numpy(np.ascontiguousarray(x)).to("cuda:0")
 
 
-@pytest.fixture(scope="module", params=[4, 2, 0], ids=["one_pass", "mixed", "auto"])
+@pytest.fixture(scope="module", params=[4, 2, 0, 8], ids=["one_pass", "mixed", "auto", "small"])
 def engine(request):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
