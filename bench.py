@@ -162,8 +162,9 @@ def parse():
     p.add_argument("--min-warm", type=int, default=500,
                    help="device pre-warm: when --warmup is below this, (min-warm - warmup) extra untimed "
                         "launches run first, over the streams, without the gather (reported as prewarm_launches)")
-    p.add_argument("--kernel", type=int, default=0,
-                   help="fs_ctx_set_kernel variant: 0 automatic, 2 mixed-length, 4 one-pass, 8 small-frame")
+    p.add_argument("--kernel", type=int, default=None,
+                   help="fs_ctx_set_kernel variant: 0 automatic, 2 mixed-length, 4 one-pass, 8 small-frame (default: "
+                        "0; --config small: 8, the variant a caller with short-frame traffic selects)")
     p.add_argument("--workgroups", type=int, default=0,
                    help="fs_ctx_set_workgroups: workgroups per launch (0: one per CU; fewer give each wave several "
                         "tiles and let consecutive launches run side by side)")
@@ -341,6 +342,8 @@ def main():
         return main_c4(args, world, rank, local, dev)
     n = args.frames or 65536
     engine = GPU.engine(local)
+    if args.kernel is None:
+        args.kernel = 8 if args.config == "small" else 0
     engine.set_kernel(args.kernel)
     if args.workgroups:
         engine.set_workgroups(args.workgroups)
@@ -598,7 +601,9 @@ def main():
                                 "traffic_calibrated divides that pattern factor out (the kernel's excess beyond it)"
                 if traffic is not None else None,
                 "kernel": {0: "automatic: digest_kernel_a (one-pass) for uniform batches, digest_kernel_ab for mixed",
-                           2: "digest_kernel_ab (mixed-length)", 4: "digest_kernel_a (one-pass)"}.get(args.kernel),
+                           2: "digest_kernel_ab (mixed-length)", 4: "digest_kernel_a (one-pass)",
+                           8: "digest_kernel_s (small-frame, one lane per frame: fs_ctx_set_kernel 8, the caller's "
+                              "choice for short-frame traffic)"}.get(args.kernel),
                 "kernel_chosen": {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine_last_kernel),
                 "kernel_avg_us": round(k_avg_ms * 1e3, 3),
                 "kernel_timing": "HIP events around K back-to-back launches on the launch stream",

@@ -210,3 +210,45 @@ def crc32_model_al(buf: bytes, S: int, length: int, base_phase: int = 0) -> int:
         Y ^= (apply(op_table(16 * a), V1) if a else V1) ^ (apply(op_table(16 * a2), V2) if a2 else V2)
     t = (4 - (E & 3)) & 3
     return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
+
+
+Z8 = op_table(8)
+
+
+def crc32_model_lane(buf: bytes, S: int, length: int, chains: int = 1) -> int:
+    """The small-frame kernel (digest_kernel_s, one lane per frame): the pending-register Horner
+    P <- Z4(P) ^ d over the frame's dwords (head/tail bytes masked, the init XOR-ed into frame
+    bytes 0..3), or with chains=2 two Horner chains over the even and the odd dwords
+    (E, O <- Z8(.) ^ d) joined at the last dword L: Z4(E) ^ O when L is odd, E ^ Z4(O) when even;
+    then the final Z_(4-t)."""
+    E_ = S + length
+    if length < 4:
+        return crc32_model(buf, S, length)
+    sa = S & 3
+    nd = (sa + length + 3) >> 2
+    te = (E_ & 3) or 4
+    head = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
+    tail = 0xFFFFFFFF if te == 4 else (1 << (8 * te)) - 1
+    padded = bytes(buf) + b"\0" * 8
+    ds = []
+    for x in range(nd):
+        d = struct.unpack_from("<I", padded, 4 * ((S >> 2) + x))[0]
+        if x == 0:
+            d &= head
+        if x == nd - 1:
+            d &= tail
+        ds.append(d ^ (head if x == 0 else (~head & 0xFFFFFFFF) if x == 1 else 0))
+    if chains == 1:
+        P = 0
+        for d in ds:
+            P = apply(Z4, P) ^ d
+    else:
+        Ev = Od = 0
+        for x, d in enumerate(ds):
+            if x & 1:
+                Od = apply(Z8, Od) ^ d
+            else:
+                Ev = apply(Z8, Ev) ^ d
+        P = (apply(Z4, Ev) ^ Od) if (nd - 1) & 1 else (Ev ^ apply(Z4, Od))
+    t = (4 - (E_ & 3)) & 3
+    return apply(ZFIN[t], P) ^ 0xFFFFFFFF

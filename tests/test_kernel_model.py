@@ -85,3 +85,20 @@ def test_block_aligned_rows_vs_zlib():
         pre = rnd.randrange(0, 70)
         buf = rnd.randbytes(pre + L + 8)
         assert km.crc32_model_al(buf, pre, L, rnd.randrange(16)) == zlib.crc32(buf[pre : pre + L])
+
+
+def test_lane_per_frame_crc_vs_zlib():
+    """The small-frame kernel's CRC (one lane per frame, one or two Horner chains) at every start
+    alignment and the lengths round the dword and chain boundaries."""
+    import random
+    import zlib
+
+    from kernel_model import crc32_model_lane
+
+    rnd = random.Random(5)
+    buf = bytes(rnd.randrange(256) for _ in range(400))
+    for S in range(8):
+        for length in list(range(0, 40)) + [47, 60, 64, 65, 127, 128, 129, 200]:
+            want = zlib.crc32(buf[S:S + length])
+            for chains in (1, 2):
+                assert crc32_model_lane(buf, S, length, chains) == want, (S, length, chains)
