@@ -1583,49 +1583,6 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             using Yes = std::true_type;
             using No = std::false_type;
             const int Rc = U.P - kPrefetch;  // first row of the last block
-            // The pass's last row was lean (unless every row was masked): if it ends the frame,
-            // its last dword -- lane 3's 4th -- still holds the up to 3 bytes past the frame end.
-            // Their CRC contribution is that junk itself (the last dword enters the combine
-            // unshifted) and their sum is sad16 of it: combine_piece removes both. (Taken from
-            // the last row before its ring slot is refilled.)
-            auto junk_of = [&](const u32x4& last) -> uint32_t {
-                uint32_t j = 0u;
-                if (pass == 0) {
-                    // mode B: a head piece ends the frame only when it is the whole frame
-                    const bool ends = npass == 1 || pieces_of(T.nd()) == 1;
-                    if (U.P > 0 && U.H < U.P && gl == 3u && T.nd() > 0 && ends) j = last.w & ~T.tail_mask();
-                } else if ((U.info & 0x40000000u) && gl == 3u) {
-                    const uint32_t t = (U.info >> 28) & 3u;
-                    j = last.w & ~(t == 0u ? 0xffffffffu : ((1u << (8u * t)) - 1u));
-                }
-                return j;
-            };
-            // The next pass's piece is set up before this pass's last block, which refills the ring
-            // with its first rows: the loads run on through the pass boundary (round 3 measured this
-            // 5% slower, when every wait in this kernel was a vmcnt(0)).
-            const bool pipe = pass + 1 < npass && U.P > 0;  // wave-uniform
-            Unit Un;
-            Un.P = 0;
-            if (pass + 1 < npass) {
-                Un = U;
-                full_piece_unit(Un, lds, ws, frames, T.F, pass + 1, grp, gl);
-            }
-            uint32_t junk = 0u;
-            auto pipe_block = [&](int r0) {
-#pragma unroll
-                for (int i = 0; i < kPrefetch; ++i) {
-                    const int r = r0 + i;
-                    const int rel = U.rel0 + kRowDwords * r;
-                    if (r < U.H) masked_row(lds, keys, pf[i], rel, load_pos(rel, U.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
-                    else lean_row(lds, keys, pf[i], A, cs);
-                    if (i == kPrefetch - 1) junk = junk_of(pf[i]);
-                    if (Un.P > 0) {
-                        const int rn = Un.rel0 + kRowDwords * i;
-                        pf[i] = load_row(Un.gfb, i < Un.H ? load_pos(rn, Un.lo) : rn);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            };
             if (U.P > 0) {
                 // [first block] (pass 0: parse) [head blocks: general] [body: lean] [last block]
                 if (Rc > 0) {
@@ -1635,12 +1592,10 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
                     int r0 = kPrefetch;
                     for (; r0 < Rc && r0 < U.H; r0 += kPrefetch) block(r0, Yes());
                     for (; r0 < Rc; r0 += kPrefetch) lean_block(r0, Yes());
-                    if (pipe) pipe_block(Rc);
-                    else if (Rc < U.H) block(Rc, No());
+                    if (Rc < U.H) block(Rc, No());
                     else lean_block(Rc, No());
                 } else {
-                    if (pipe) pipe_block(0);
-                    else if (U.H > 0) block(0, No());
+                    if (U.H > 0) block(0, No());
                     else lean_block(0, No());
                     if (pass == 0) parse(false);
                 }
@@ -1651,12 +1606,24 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             // Opaque frame descriptor: what the combine and the finish derive from it is
             // recomputed here rather than kept (and spilled) across the row loop.
             asm volatile("" : "+v"(T.S), "+v"(T.len));
-            if (!pipe) junk = junk_of(pf[kPrefetch - 1]);
+            // The pass's last row was lean (unless every row was masked): if it ends the frame,
+            // its last dword -- lane 3's 4th -- still holds the up to 3 bytes past the frame end.
+            // Their CRC contribution is that junk itself (the last dword enters the combine
+            // unshifted) and their sum is sad16 of it: combine_piece removes both.
+            uint32_t junk = 0u;
+            if (pass == 0) {
+                // mode B: a head piece ends the frame only when it is the whole frame
+                const bool ends = npass == 1 || pieces_of(T.nd()) == 1;
+                if (U.P > 0 && U.H < U.P && gl == 3u && T.nd() > 0 && ends) junk = pf[kPrefetch - 1].w & ~T.tail_mask();
+            } else if ((U.info & 0x40000000u) && gl == 3u) {
+                const uint32_t t = (U.info >> 28) & 3u;
+                junk = pf[kPrefetch - 1].w & ~(t == 0u ? 0xffffffffu : ((1u << (8u * t)) - 1u));
+            }
             const uint32_t info = U.info;
-            // the next pass's piece (its first rows in flight during this pass's combine)
+            // the next pass's piece and its first rows, in flight during this pass's combine
             if (pass + 1 < npass) {
-                U = Un;
-                if (!pipe) prefetch_unit(U, pf);
+                full_piece_unit(U, lds, ws, frames, T.F, pass + 1, grp, gl);
+                prefetch_unit(U, pf);
             }
             uint32_t y, c;
             combine_piece(lds, gl, A, cs, junk, y, c);

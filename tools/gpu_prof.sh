@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 cd /tmp
 for cfg in c2 c3; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof/$cfg" -o run -- \
-    python3 "$R/bench.py" --config $cfg --cpu-seconds 10 > "$R/gpurun_out/prof/bench_$cfg.json" 2> "$R/gpurun_out/prof/bench_$cfg.err" \
+    python3 "$R/bench.py" --config $cfg --cpu-seconds 10 --no-sub > "$R/gpurun_out/prof/bench_$cfg.json" 2> "$R/gpurun_out/prof/bench_$cfg.err" \
     || { echo "rocprof bench $cfg failed"; tail -5 "$R/gpurun_out/prof/bench_$cfg.err"; exit 1; }
   tail -1 "$R/gpurun_out/prof/bench_$cfg.json"
 done
