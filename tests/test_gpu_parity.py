@@ -362,6 +362,33 @@ def test_few_workgroups(engine, workgroups):
         engine.set_workgroups(0)
 
 
+def test_prepared_calls_match(engine):
+    """Engine.prepare_digest (checked and marshalled once, the bench's path) gives what
+    digest_device gives, call after call, for the RX digest and the FCS verify."""
+    import framegen
+
+    dev = torch.device("cuda:0")
+    frames = framegen.edge_batch(21, n_random=500)
+    buf, off, ln = pack_frames(frames, align=4)
+    tb, to, tl = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (buf, off.astype(np.int64),
+                                                                             ln.astype(np.int32)))
+    ref_out, ref_st = engine.digest_device(tb, to, tl, mtu=1514)
+    out = torch.empty_like(ref_out)
+    st = torch.empty_like(ref_st)
+    s = torch.cuda.Stream(dev)
+    call = engine.prepare_digest(tb, to, tl, mtu=1514, out=out, status=st, stream=s)
+    for _ in range(3):
+        out.fill_(0)
+        st.fill_(0xFF)
+        o, v = call()
+        assert o is out and v is st
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref_out) and torch.equal(st, ref_st)
+    dig, est = coracle.digest_batch(buf, off, ln, mtu=1514)
+    crc, ipc, l4c = split_digests(out.cpu().numpy())
+    assert np.array_equal(crc, dig["crc32"]) and np.array_equal(st.cpu().numpy(), est)
+
+
 def test_set_workgroups_rejects_negative():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
