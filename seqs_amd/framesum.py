@@ -298,6 +298,8 @@ class Engine:
         keep = (frames, offsets, lengths, out, status, stream)
 
         def call():
+            if self._ctx is None:  # (the context was closed: its pointer in `args` is gone)
+                raise FramesumError(f"{name}: the engine was closed")
             st = fn(*args)
             if st:
                 self._check(st, name)
