@@ -56,6 +56,12 @@ class FakeEngine:
 
     digest_fcs_device = digest_device
 
+    def prepare_digest(self, frames, offsets, lengths, mtu=0, out=None, status=None, stream=None, op="digest",
+                       flags=1):
+        # the bench's prepared-call path (Engine.prepare_digest): one closure per (batch, slot, stream)
+        self.prepared = getattr(self, "prepared", 0) + 1
+        return lambda: self.digest_device(frames, offsets, lengths, mtu, out, status, stream)
+
     def fill_device(self, frames, offsets, lengths, flags=0, mtu=0, out=None, status=None, stream=None):
         return self.digest_device(frames, offsets, lengths, mtu, out, status, stream)
 
