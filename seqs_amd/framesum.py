@@ -235,7 +235,7 @@ class Engine:
         self._check(self.lib.fs_ctx_set_workgroups(self._ctx, int(workgroups)), "fs_ctx_set_workgroups")
 
     def last_kernel(self) -> int:
-        """The variant (2 or 4) this context's latest launch ran (0 before its first launch). With
+        """The variant (2, 4 or 8) this context's latest launch ran (0 before its first launch). With
         variant 0 the first 16 launches run the mixed-length kernel (2); it stays chosen while its
         batches have mixed-length tiles, uniform traffic then moves to the one-pass kernel (4)."""
         v = self.lib.fs_ctx_last_kernel(self._ctx)
