@@ -659,9 +659,18 @@ def single_gpu_region(engine, batches, steps: int, warmup: int, min_warm: int, n
     streams = [GPU.stream(dev) for _ in range(ns)]
     nb = len(batches)
 
+    # prepared calls per (batch, slot, stream), as the headline's steps (a step of the small-frame
+    # record is ~5 us: the host's per-call marshalling would otherwise pace it)
+    prepared = {}
+
     def launch(i, s):
-        fb, fo, fl = batches[i % nb]
-        engine.digest_device(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot], stream=s)
+        key = (i % nb, i % nslot, id(s))
+        f = prepared.get(key)
+        if f is None:
+            fb, fo, fl = batches[i % nb]
+            f = prepared[key] = engine.prepare_digest(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot],
+                                                      stream=s)
+        f()
 
     for i in range(max(0, min_warm - warmup)):
         launch(i, streams[i % ns])
