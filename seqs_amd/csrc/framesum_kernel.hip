@@ -1196,8 +1196,9 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     // Preamble: the first tile's descriptors (the first memory ops, one round trip) while the
     // tables are built in place by VALU; geometry; the first rows; the masked-row count and the
     // capture flag; one barrier once this wave's table stores are done.
-    // (not readfirstlane'd: the wave-uniform form took 128 VGPRs against 118 and measured ~1% slower
-    // on C2, profiles/round4/session2/ab_pipelined_variants.jsonl)
+    // (round 4 built a pipelined tile transition -- the next tile's descriptors during the rows, its
+    // first rows in the last block -- and measured it 3-5% slower on two-tile batches and 1-2% on C4,
+    // equal on C2: DESIGN.md §3.11; this loop stays)
     uint32_t tile = gwave;
     FS_RTSTAMP(5);
     FS_STAMP(0);
@@ -1314,94 +1315,25 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
-        // the last block when the wave has a next tile with rows: the same consumption, and its
-        // refills are that tile's first kPfA rows (the ring runs on through the transition)
-        auto next_block = [&](int r0, const TileA& Tn) {
-            prio(r0);
-#pragma unroll
-            for (int i = 0; i < kPfA; ++i) {
-                const int r = r0 + i;
-                const int rel = T.rel0 + kRowDwords * r;
-                if (r < T.H) masked_row_al<Lay::kRegion>(lds, keys, pf[i], rel, T.nd(), T.sa(), T.tail_mask(), A, cs);
-                else if (i == kPfA - 1) tail_row_al<Lay::kRegion>(lds, keys, pf[i], rel, T.nd(), T.tail_mask(), A, cs);
-                else lean_row<Lay::kRegion>(lds, keys, pf[i], A, cs);
-                if (r0 == 0 && T.cap) {  // (a one-block tile: its first blocks into the header slot)
-                    const uint32_t k = (uint32_t)(i - T.r0f);
-                    if (k < (uint32_t)Lay::kCapBlocks) {
-                        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-                        const u32x4 v = pf[i];
-                        const bool s1 = (gl & 1u) != 0u;
-                        const u32x2 h0 = s1 ? u32x2{v.z, v.w} : u32x2{v.x, v.y};
-                        const u32x2 h1 = s1 ? u32x2{v.x, v.y} : u32x2{v.z, v.w};
-                        const uint32_t cb = hw + (4u * k + gl) * 256u + grp * 16u + ((gl & 1u) << 3);
-                        *reinterpret_cast<u32x2*>(lds + cb) = h0;
-                        *reinterpret_cast<u32x2*>(lds + (cb ^ 8u)) = h1;
-                    }
-                }
-                const int rn = Tn.rel0 + kRowDwords * i;
-                pf[i] = load_row(Tn.gfb, i < Tn.H ? lpos(rn, Tn.lo) : rn);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        };
         using Yes = std::true_type;
         using No = std::false_type;
-        // The wave's next tile (a batch of more tiles than waves, or a launch of fewer workgroups):
-        // its descriptors are loaded during this tile's rows, its geometry computed before this
-        // tile's last block, and that block refills the ring with its first rows, so the
-        // transition waits for no memory round trip (the combine and finish below overlap them).
-        const uint32_t ntile = tile + nwaves;
-        const bool has_next = ntile < ntiles;  // wave-uniform
-        TileA Tn;
-        Tn.P = 0;
-        uint64_t Sn = 0;
-        uint32_t lenn = 0;
-        // wait for the next tile's descriptors (`older`: kPfA ring loads issued after them) and
-        // derive its geometry
-        auto next_geometry = [&](bool older) {
-            if (older) asm volatile("s_waitcnt vmcnt(%2)" : "+v"(Sn), "+v"(lenn) : "n"(kPfA));
-            else asm volatile("s_waitcnt vmcnt(0)" : "+v"(Sn), "+v"(lenn));
-            if (kOps == kOpsFcs) lenn = lenn >= 4u ? lenn - 4u : 0u;
-            tile_geometry_a<Lay::kCapBlocks>(Tn, ntile, grp, gl, n, Sn, lenn, frames, fpt);
-            if (report && mode_b_worthy(Tn.nd()) && lane == 0u) post_report(report);
-        };
         if (T.P > 0) {
-            // [first block] parse [head blocks: general] [body: lean] [last block: no refill, or
-            // the next tile's first rows]
+            // [first block] parse [head blocks: general] [body: lean] [last block: no refill]
             if (Rc > 0) {
                 if (T.H > 0) block(0, Yes());
                 else lean_block(0, Yes());
-                // the next tile's descriptors: behind this block's refills (older than every later one)
-                if (has_next) tile_descriptors(ntile, grp, n, offsets, lengths, Sn, lenn, fpt);
                 parse();
                 int r0 = kPfA;
                 for (; r0 < Rc && r0 < T.H; r0 += kPfA) block(r0, Yes());
                 for (; r0 < Rc; r0 += kPfA) lean_block(r0, Yes());
-                if (has_next) next_geometry(Rc >= 2 * kPfA);
-                if (Tn.P > 0) next_block(Rc, Tn);
-                else if (Rc < T.H) block(Rc, No());
+                if (Rc < T.H) block(Rc, No());
                 else lean_block(Rc, No());
             } else {
-                if (has_next) {
-                    tile_descriptors(ntile, grp, n, offsets, lengths, Sn, lenn, fpt);
-                    next_geometry(false);
-                }
-                if (Tn.P > 0) next_block(0, Tn);
-                else if (T.H > 0) block(0, No());
+                if (T.H > 0) block(0, No());
                 else lean_block(0, No());
                 parse();
             }
         } else {
-            if (has_next) {
-                tile_descriptors(ntile, grp, n, offsets, lengths, Sn, lenn, fpt);
-                next_geometry(false);
-                if (Tn.P > 0) {
-#pragma unroll
-                    for (int i = 0; i < kPfA; ++i) {
-                        const int rel = Tn.rel0 + kRowDwords * i;
-                        pf[i] = load_row(Tn.gfb, i < Tn.H ? lpos(rel, Tn.lo) : rel);
-                    }
-                }
-            }
             parse();  // no rows (every frame of the tile under 4 bytes): rejected by length
         }
         FS_STAMP(2);
@@ -1445,9 +1377,21 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                                     status, tx);
         FS_STAMP(4);
         FS_RTSTAMP(6);
-        tile = ntile;
-        if (has_next) {  // the next tile's rows are in flight; its header slots (this tile's are done)
-            T = Tn;
+        tile += nwaves;
+        if (tile < ntiles) {  // next tile: descriptors, geometry, row prefetch, header slots
+            uint64_t S;
+            uint32_t len;
+            tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
+            descriptors_ready<kOps>(S, len);
+            tile_geometry_a<Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
+            if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+            if (T.P > 0) {
+#pragma unroll
+                for (int i = 0; i < kPfA; ++i) {
+                    const int rel = T.rel0 + kRowDwords * i;
+                    pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
+                }
+            }
             tile_header(T);
         }
     }

@@ -329,7 +329,7 @@ def test_many_tiles_per_wave(engine, n, flen):
 
 def _tile_mix_batch(ntiles: int, seed: int):
     """Tiles of 16 frames, each tile one random length class, so a wave streaming several tiles
-    meets every transition of the one-pass kernel's pipelined tile loop: tiles of frames under 4
+    meets every transition of the one-pass kernel's tile loop: tiles of frames under 4
     bytes (no rows), one-block tiles (<= 5 blocks), two-block tiles, MTU and jumbo tiles, tiles of
     widely mixed lengths (header slots loaded, not captured) and a partial last tile."""
     rng = np.random.default_rng(seed)
@@ -349,8 +349,8 @@ def _tile_mix_batch(ntiles: int, seed: int):
 
 @pytest.mark.parametrize("workgroups", [1, 7, 64])
 def test_few_workgroups(engine, workgroups):
-    """fs_ctx_set_workgroups: a capped grid gives each wave many tiles, streamed back to back (the
-    next tile's descriptors and first rows are in flight during the current tile's last block)."""
+    """fs_ctx_set_workgroups: a capped grid gives each wave many tiles, streamed back to back (every
+    transition between tile classes: no rows, one- and two-block tiles, MTU, jumbo, mixed)."""
     engine.set_workgroups(workgroups)
     try:
         buf, off, ln = synth.uniform_batch(20000, 1500, seed=workgroups)
