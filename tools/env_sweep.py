@@ -21,6 +21,8 @@ SETTINGS = [
     ("DEBUG_CLR_KERNARG_HDP_FLUSH_WA=0", {"DEBUG_CLR_KERNARG_HDP_FLUSH_WA": "0"}, []),
     ("streams=3", {}, ["--streams", "3"]),
     ("streams=4", {}, ["--streams", "4"]),
+    ("streams=6", {}, ["--streams", "6"]),
+    ("streams=7", {}, ["--streams", "7"]),
     ("streams=8", {}, ["--streams", "8"]),
     ("wg=192", {}, ["--workgroups", "192"]),
     ("wg=128", {}, ["--workgroups", "128"]),
