@@ -1617,7 +1617,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 
 
 // =======================================================================================
-// The small-frame kernel (digest_kernel_s, variant 8; DESIGN.md §3.11): ONE LANE PER FRAME,
+// The small-frame kernel (digest_kernel_s, variant 8; DESIGN.md §3.12): ONE LANE PER FRAME,
 // 64 frames per wave, for batches of short frames (the reference's own benchmark sends 47-byte
 // UDP frames, stacks/benchmark_test.go:12-46). The 4-lane kernels spend a 104-KB table image,
 // a workgroup barrier and one 16-wave workgroup per CU on every launch; on 47-byte frames that
