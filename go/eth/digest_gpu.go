@@ -99,6 +99,23 @@ func (g *GPU) Close() error {
 
 func (g *GPU) lastErr() error { return errors.New("framesum: " + C.GoString(C.fs_last_error(g.ctx))) }
 
+// Kernel variants of fs_ctx_set_kernel (include/framesum.h): results never depend on them.
+const (
+	KernelAuto    = 0 // one-pass kernel for uniform lengths, piece-splitting kernel for mixed ones
+	KernelMixed   = 2 // piece-splitting kernel
+	KernelOnePass = 4 // one-pass kernel
+	KernelSmall   = 8 // one lane per frame: a stack whose traffic is short frames (ACKs, DNS, DHCP,
+	// the reference's 47-byte benchmark frames in stacks/benchmark_test.go)
+)
+
+// SetKernel selects the kernel variant of this context's launches (fs_ctx_set_kernel).
+func (g *GPU) SetKernel(variant int) error {
+	if st := C.fs_ctx_set_kernel(g.ctx, C.int(variant)); st != C.FS_SUCCESS {
+		return g.lastErr()
+	}
+	return nil
+}
+
 // stage packs frames back to back, each at a 4-byte aligned offset, into pinned memory,
 // followed by 16 spare bytes (slack for the dword-rounded copy span; on the device the engine
 // reads the 64-byte blocks around each frame inside its own staging buffer). The

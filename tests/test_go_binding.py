@@ -33,7 +33,8 @@ def test_go_files_declare_the_binding():
     for sym in ("func OpenGPU(", "func (g *GPU) DigestBatch(", "func (g *GPU) FillBatch(", "func OpenGPUs(",
                 "func (m *GPUs) DigestBatch(", "C.fs_digest_batch_host(", "C.fs_fill_batch_host(",
                 "C.fs_digest_batch_multi(", "C.fs_host_alloc(", "func OpenGroup(", "func (g *Group) DigestSharded(",
-                "func ShardCount(", "C.fs_group_create(", "C.fs_digest_batch_sharded(", "C.fs_shard_count("):
+                "func ShardCount(", "C.fs_group_create(", "C.fs_digest_batch_sharded(", "C.fs_shard_count(",
+                "func (g *GPU) SetKernel(", "C.fs_ctx_set_kernel("):
         assert sym in eth, sym
     for sym in ("func (ps *PortStack) RecvEthBatch(", "func (ps *PortStack) recvEthVerified(", "deliverUDP", "deliverTCP"):
         assert sym in stacks, sym
@@ -43,6 +44,9 @@ def test_go_files_declare_the_binding():
     c = {int(v) for _, v in re.findall(r"(FS_[A-Z0-9_]+)\s*=\s*(\d+)", hdr)}
     go = {int(v) for v in re.findall(r"Verdict[A-Za-z0-9]+\s+Verdict = (\d+)", eth)}
     assert go == c
+    # the Go kernel-variant constants are the values fs_ctx_set_kernel accepts
+    kv = {int(v) for v in re.findall(r"Kernel[A-Za-z]+\s+= (\d+)", eth)}
+    assert kv == {0, 2, 4, 8}
 
 
 def write_list(path, frames):
