@@ -150,7 +150,9 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
 /* Same computation from/to HOST memory (the NIC / loopback buffer handed to
  * RecvEth): stages H2D, runs the kernel and copies D2H on the context's
  * stream, returning when the results are in `out`/`status`. Pinned memory
- * (fs_host_alloc) gives full PCIe rate; pageable memory works. */
+ * (fs_host_alloc) gives full PCIe rate; pageable memory works. With the automatic
+ * kernel choice (fs_ctx_set_kernel 0) a batch whose frames are all <= 128 bytes runs
+ * the small-frame kernel (variant 8): the lengths are on the host here. */
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status);
 

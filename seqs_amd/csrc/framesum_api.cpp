@@ -154,14 +154,21 @@ fs_status quiesce_host_streams(fs_ctx* ctx) {
 }
 
 // One launch of the context's kernel choice.
+// `force` < 0: the context's kernel choice (fs_ctx_set_kernel).
 hipError_t launch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                   uint32_t mtu, fs_digest* out, uint8_t* status, hipStream_t stream, framesum::FsOp op,
-                  uint8_t* wframes, uint32_t tx) {
+                  uint8_t* wframes, uint32_t tx, int force = -1) {
     const int wgs = ctx->workgroups > 0 && ctx->workgroups < ctx->num_cus ? ctx->workgroups : ctx->num_cus;
     return framesum::launch_digest(frames, offsets, lengths, n, mtu, ctx->d_tables, out, status, stream, wgs,
-                                   ctx->h_report, ctx->d_report, &ctx->next_launch_id, ctx->force_kernel, op, wframes,
-                                   tx);
+                                   ctx->h_report, ctx->d_report, &ctx->next_launch_id,
+                                   force >= 0 ? force : ctx->force_kernel, op, wframes, tx);
 }
+
+// The host-staged digest sees the batch's lengths on the host: with the automatic choice, a batch
+// whose frames are all this short runs the small-frame kernel (variant 8, one lane per frame; its
+// header slot holds frames up to ~130 B). A device-resident batch's lengths are in device memory:
+// there the caller selects it (fs_ctx_set_kernel).
+constexpr uint32_t kSmallAutoMaxLen = 128;
 
 }  // namespace
 
@@ -315,9 +322,11 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: null pointer");
-    const uint32_t bad = framesum::plan::first_frame_out_of_range(offsets, lengths, n, frames_bytes);
+    uint32_t max_len = 0;
+    const uint32_t bad = framesum::plan::first_frame_out_of_range(offsets, lengths, n, frames_bytes, 0, &max_len);
     if (bad < n)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(bad) + " ends past frames_bytes");
+    const int force = ctx->force_kernel == 0 && max_len <= kSmallAutoMaxLen ? 8 : ctx->force_kernel;
     FS_HIP(ctx, hipSetDevice(ctx->device));
     fs_status pst = quiesce_host_streams(ctx);
     if (pst != FS_SUCCESS) return pst;
@@ -383,7 +392,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         // the kernel addresses frame i at base + offsets[i]: base = staging - cpy_lo (4-B aligned)
         const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
         FS_HIP(ctx, launch(ctx, base, d_off + c0, d_len + c0, cnt, mtu, sl.d_out, status ? sl.d_status : nullptr, ks,
-                           framesum::FsOp::kDigest, nullptr, 0));
+                           framesum::FsOp::kDigest, nullptr, 0, force));
         FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
         sl.used = true;
         FS_HIP(ctx, hipMemcpyAsync(h_out + c0, sl.d_out, (size_t)cnt * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));

@@ -91,11 +91,14 @@ inline void chunk_plan(uint64_t n, uint32_t N, uint32_t nchunks_max, uint64_t ta
 
 // Index of the first frame that does not lie inside [0, frames_bytes) (overflow-safe), or n.
 inline uint32_t first_frame_out_of_range(const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
-                                         uint64_t frames_bytes, uint32_t extra = 0) {
+                                         uint64_t frames_bytes, uint32_t extra = 0, uint32_t* max_len = nullptr) {
+    uint32_t mx = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint64_t need = (uint64_t)lengths[i] + extra;
         if (offsets[i] > frames_bytes || need > frames_bytes - offsets[i]) return i;
+        mx = lengths[i] > mx ? lengths[i] : mx;
     }
+    if (max_len) *max_len = mx;  // (the batch's longest frame, when every frame is in range)
     return n;
 }
 

@@ -389,6 +389,35 @@ def test_prepared_calls_match(engine):
     assert np.array_equal(crc, dig["crc32"]) and np.array_equal(st.cpu().numpy(), est)
 
 
+def test_host_path_picks_small_kernel():
+    """fs_digest_batch_host sees the lengths on the host: with the automatic choice a batch whose
+    frames are all <= 128 B runs the small-frame kernel (variant 8), any longer frame keeps the
+    4-lane kernels; results match the oracle either way."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    e = Engine(0)
+    try:
+        buf, off, ln = synth.hello_batch(5000, seed=9)
+        dig, st = e.digest_host(buf, off, ln)
+        assert e.last_kernel() == 8
+        edig, est = coracle.digest_batch(buf, off, ln)
+        assert np.array_equal(dig["crc32"], edig["crc32"]) and np.array_equal(st, est)
+        assert np.array_equal(dig["l4_csum"], edig["l4_csum"]) and (st == 0).all()
+        import framegen
+        frames = framegen.edge_batch(33, n_random=300)
+        b2, o2, l2 = pack_frames(frames, align=4)
+        assert int(l2.max()) > 128
+        dig2, st2 = e.digest_host(b2, o2, l2, mtu=1514)
+        assert e.last_kernel() in (2, 4)
+        edig2, est2 = coracle.digest_batch(b2, o2, l2, mtu=1514)
+        assert np.array_equal(dig2["crc32"], edig2["crc32"]) and np.array_equal(st2, est2)
+        e.set_kernel(4)  # a forced choice wins
+        e.digest_host(buf, off, ln)
+        assert e.last_kernel() == 4
+    finally:
+        e.close()
+
+
 def test_set_workgroups_rejects_negative():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
