@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Host-staged (PCIe-inclusive) rate of the reference's benchmark shape (65,536 x 47-B UDP frames,
+stacks/benchmark_test.go): fs_digest_batch_host with the automatic choice (the small-frame kernel:
+every frame <= 128 B) against the one-pass kernel forced, alternated. Measurement tool; never the
+bench value."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from seqs_amd import Engine, synth  # noqa: E402
+
+
+def main():
+    eng = Engine(0)
+    buf, off, ln = synth.hello_batch(65536, seed=3)
+    pinned = eng.host_empty(buf.shape, np.uint8)
+    pinned[:] = buf
+    n, nbytes = len(ln), int(ln.astype(np.int64).sum())
+    res = {}
+    for rnd in range(3):
+        for name, k in (("auto (small-frame kernel)", 0), ("one-pass forced", 4)):
+            eng.set_kernel(k)
+            for _ in range(20):
+                eng.digest_host(pinned, off, ln)
+            reps = 200
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                _, st = eng.digest_host(pinned, off, ln)
+            el = (time.perf_counter() - t0) / reps
+            assert (st == 0).all()
+            res.setdefault(name, []).append((el, eng.last_kernel()))
+    for name, v in res.items():
+        els = sorted(x[0] for x in v)
+        print(json.dumps({"case": "65536 x 47-B UDP, fs_digest_batch_host (pinned)", "kernel": name,
+                          "last_kernel": v[-1][1], "us_per_call": [round(x * 1e6, 1) for x in els],
+                          "Mframes_s_best": round(n / els[0] / 1e6, 1),
+                          "GiB_s_best": round(nbytes / els[0] / 2**30, 2)}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
