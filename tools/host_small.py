@@ -20,6 +20,8 @@ def main():
     pinned = eng.host_empty(buf.shape, np.uint8)
     pinned[:] = buf
     n, nbytes = len(ln), int(ln.astype(np.int64).sum())
+    from oracle import coracle  # the checker only (a random source port can be 0: ErrZeroPort)
+    _, est = coracle.digest_batch(buf, off, ln)
     res = {}
     for rnd in range(3):
         for name, k in (("auto (small-frame kernel)", 0), ("one-pass forced", 4)):
@@ -31,7 +33,7 @@ def main():
             for _ in range(reps):
                 _, st = eng.digest_host(pinned, off, ln)
             el = (time.perf_counter() - t0) / reps
-            assert (st == 0).all()
+            assert np.array_equal(st, est)
             res.setdefault(name, []).append((el, eng.last_kernel()))
     for name, v in res.items():
         els = sorted(x[0] for x in v)
