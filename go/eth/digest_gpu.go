@@ -101,7 +101,8 @@ func (g *GPU) lastErr() error { return errors.New("framesum: " + C.GoString(C.fs
 
 // Kernel variants of fs_ctx_set_kernel (include/framesum.h): results never depend on them.
 const (
-	KernelAuto    = 0 // one-pass kernel for uniform lengths, piece-splitting kernel for mixed ones
+	KernelAuto    = 0 // one-pass kernel for uniform lengths, piece-splitting kernel for mixed ones;
+	// DigestBatch picks KernelSmall itself for a batch of frames all <= 128 B
 	KernelMixed   = 2 // piece-splitting kernel
 	KernelOnePass = 4 // one-pass kernel
 	KernelSmall   = 8 // one lane per frame: a stack whose traffic is short frames (ACKs, DNS, DHCP,
