@@ -15,6 +15,7 @@
 package stacks
 
 import (
+	"errors"
 	"io"
 	"log/slog"
 
@@ -68,6 +69,11 @@ var verdictErr = [...]error{
 	eth.VerdictBadTCPOffset:       errBadTCPOffset,
 	eth.VerdictChecksum:           ErrChecksumTCPorUDP,
 }
+
+// errUnexpectedVerdict: a frame reached the delivery step with a verdict that is not
+// VerdictOK and that no earlier step ends the frame on (VerdictFCS, a value this file does not
+// know, a corrupted status byte). Such a frame is never handed to a socket: fail closed.
+var errUnexpectedVerdict = errors.New("stacks: RecvEthBatch: unexpected GPU verdict")
 
 // gateKind is one step of RecvEth's decision order (portstack.go:163-355) once the GPU has
 // evaluated a frame's byte-level gates. recvEthVerified walks recvEthGates in order; the order
@@ -174,6 +180,9 @@ func (ps *PortStack) recvEthVerified(frame []byte, v eth.Verdict) error {
 				return nil // RecvEth stops before its L4 gates
 			}
 		case gateDeliver:
+			if v != eth.VerdictOK { // fail closed: only a verified frame reaches a socket
+				return errUnexpectedVerdict
+			}
 			offset := eth.SizeEthernetHeader + int(ipOffset)
 			segment := frame[offset : eth.SizeEthernetHeader+int(ihdr.TotalLength)]
 			var err error

@@ -30,6 +30,8 @@ struct fs_group {
     uint8_t* recv = nullptr;     // first device: n slabs back to back
     uint64_t cap_slab = 0;       // bytes per slab currently allocated
     long fault_chunk = -1;       // test library only (fs_test_group_set_fault): fail at this chunk
+    long fault_gather = -1;      // test library only (fs_test_group_set_fault_gather): an RCCL error here
+    bool aborted = false;        // an RCCL error aborted the communicators: the group is unusable
     std::string err;
 };
 
@@ -97,6 +99,23 @@ void quiesce_group(fs_group* g) {
 fs_status fail_group(fs_group* g, fs_status code, const std::string& msg) {
     quiesce_group(g);
     return gset(g, code, msg);
+}
+
+// An RCCL error after part of a chunk's grouped sends and receives may have been enqueued: a send
+// whose receive never comes would keep its transfer stream busy forever, so synchronizing that
+// stream could hang. The communicators are aborted first (ncclCommAbort ends their pending
+// operations and frees them), then the streams are drained. The group stays unusable: every later
+// call fails until it is destroyed and created again.
+fs_status fail_group_comm(fs_group* g, const std::string& msg) {
+    for (int k = 0; k < g->n; ++k) {
+        if (!g->comm[k]) continue;
+        (void)hipSetDevice(g->dev[k]);
+        (void)ncclCommAbort(g->comm[k]);
+        g->comm[k] = nullptr;
+    }
+    g->aborted = true;
+    quiesce_group(g);
+    return gset(g, FS_E_HIP, msg + " (the group's RCCL communicators were aborted: destroy the group and create it again)");
 }
 
 }  // namespace
@@ -194,6 +213,13 @@ fs_status fs_test_group_set_fault(fs_group* g, long chunk) {
     g->fault_chunk = chunk;
     return FS_SUCCESS;
 }
+// ... and at chunk `chunk`'s gather, after its grouped sends and receives are enqueued, as if RCCL
+// had failed there (the communicator-abort path).
+fs_status fs_test_group_set_fault_gather(fs_group* g, long chunk) {
+    if (!g) return FS_E_INVALID;
+    g->fault_gather = chunk;
+    return FS_SUCCESS;
+}
 #endif
 
 
@@ -203,6 +229,9 @@ fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, con
                                   uint8_t* status) {
     if (!g) return FS_E_INVALID;
     g->err.clear();
+    if (g->aborted)
+        return gset(g, FS_E_HIP, "fs_digest_batch_sharded: the group's RCCL communicators were aborted by an earlier "
+                                 "error: destroy the group and create it again");
     if (n == 0) return FS_SUCCESS;
     if (!frames || !offsets || !lengths || !out) return gset(g, FS_E_INVALID, "fs_digest_batch_sharded: null pointer");
     const uint32_t N = (uint32_t)g->n;
@@ -256,10 +285,12 @@ fs_status fs_digest_batch_sharded(fs_group* g, const uint8_t* const* frames, con
             if (r == ncclSuccess) r = ncclRecv(g->recv + p.recv_dig, 8 * p.rows, ncclUint8, (int)k, g->comm[0], g->xfer[0]);
             if (r == ncclSuccess) r = ncclRecv(g->recv + p.recv_st, p.rows, ncclUint8, (int)k, g->comm[0], g->xfer[0]);
         }
-        const ncclResult_t r2 = ncclGroupEnd();
+        ncclResult_t r2 = ncclGroupEnd();
+        if ((long)c == g->fault_gather && r == ncclSuccess && r2 == ncclSuccess)
+            r2 = ncclInternalError;  // test library only: the chunk's transfers are enqueued here
         if (r != ncclSuccess || r2 != ncclSuccess)
-            return fail_group(g, FS_E_HIP, std::string("fs_digest_batch_sharded: chunk gather: ") +
-                                               ncclGetErrorString(r != ncclSuccess ? r : r2));
+            return fail_group_comm(g, std::string("fs_digest_batch_sharded: chunk gather: ") +
+                                          ncclGetErrorString(r != ncclSuccess ? r : r2));
         e = hipSetDevice(g->dev[0]);
         if (e == hipSuccess) e = framesum::launch_deinterleave(g->recv, N, n, out, status, g->xfer[0], x.g0, x.g1);
         if (e != hipSuccess) break;

@@ -1701,11 +1701,14 @@ digest_kernel_s(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         const uint32_t fi = tile * 64u + lane;
         const bool valid = fi < n;
         if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
-        const uint32_t sa = (uint32_t)S & 3u;
-        const uint32_t xo = (uint32_t)(S >> 2) & 3u;  // frame dword 0's place in its 16-B chunk
+        // 16-B chunks at ABSOLUTE 16-B boundaries (frames is only 4-byte aligned): a chunk that
+        // holds a frame byte never leaves that byte's page
+        const uint64_t fa = reinterpret_cast<uint64_t>(frames) + S;
+        const uint32_t sa = (uint32_t)fa & 3u;        // = S & 3 (frames is 4-byte aligned)
+        const uint32_t xo = (uint32_t)(fa >> 2) & 3u;  // frame dword 0's place in its 16-B chunk
         const uint32_t nd = (sa + len + 3u) >> 2;     // dwords holding frame bytes
         const uint32_t nch = valid && len > 0u ? (xo + nd + 3u) >> 2 : 0u;
-        const u32x4* cb = reinterpret_cast<const u32x4*>(frames + ((S >> 4) << 4));
+        const u32x4* cb = reinterpret_cast<const u32x4*>(fa & ~(uint64_t)15u);
         // the frame's chunks into the slot (the chunks past the slot come from memory below)
         u32x4 v[kSmallSlotRows];
 #pragma unroll
@@ -1828,10 +1831,11 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
             mixed = true;
         }
     }
-    if (force) mixed = force == 2;  // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
-    // 8: the small-frame kernel (RX digest and FCS verify; a TX fill runs the automatic choice)
+    // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel, 8 the small-frame kernel
+    // (RX digest and FCS verify; a TX fill keeps the automatic choice above)
+    if (force == 2 || force == 4) mixed = force == 2;
     const bool small = force == 8 && op != FsOp::kFill;
-    if (force == 8) mixed = false;
+    if (small) mixed = false;
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {
         if (report_host) report_host[kReportChosen] = v;

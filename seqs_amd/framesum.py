@@ -166,6 +166,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.fs_test_set_fault.argtypes = [vp, ctypes.c_long]
         lib.fs_test_group_set_fault.restype = i32
         lib.fs_test_group_set_fault.argtypes = [vp, ctypes.c_long]
+        lib.fs_test_group_set_fault_gather.restype = i32
+        lib.fs_test_group_set_fault_gather.argtypes = [vp, ctypes.c_long]
     _libs[p] = lib
     if path is None:
         _lib = lib

@@ -187,7 +187,8 @@ def recv_eth_batch_table(f: bytes, v: int, ps: Stack, gates, verr):
             if (f[23] == 17 and ps.udp == 0) or (f[23] == 6 and ps.tcp == 0):
                 return ("nil", "nosock")
         elif kind == "gateDeliver":
-            assert v == 0, f"a frame reached the delivery with verdict {v}"
+            if v != 0:  # fail closed (go_deliver_fails_closed pins that the Go step does this)
+                return ("err", "errUnexpectedVerdict")
             ipoff = (f[14] & 0xF) * 4
             dport = struct.unpack(">H", f[14 + ipoff + 2: 14 + ipoff + 4])[0]
             ports = ps.udp if f[23] == 17 else ps.tcp
@@ -245,3 +246,39 @@ def test_recv_eth_batch_gate_order_matches_recv_eth(mtu):
               "errUnknownIPProto", "errTooShortTCPOrUDP", "errZeroPort", "ErrChecksumTCPorUDP", "glob"):
         assert k in kinds, f"no frame reached {k}"
     assert checked > 10000
+
+
+def go_deliver_fails_closed():
+    """The gateDeliver case of recvEthVerified returns errUnexpectedVerdict for any verdict other
+    than VerdictOK before it touches the segment (fail closed)."""
+    src = open(GO_BATCH).read()
+    body = re.search(r"case gateDeliver:\n(.*?)\n\t\t\}\n\t\}", src, re.S).group(1)
+    first = [ln.strip() for ln in body.splitlines() if ln.strip()][:2]
+    return first == ["if v != eth.VerdictOK { // fail closed: only a verified frame reaches a socket",
+                     "return errUnexpectedVerdict"]
+
+
+def test_deliver_step_fails_closed_in_go_source():
+    assert go_deliver_fails_closed()
+
+
+@pytest.mark.parametrize("v", [14, 15, 63, 255])
+def test_verdicts_outside_the_table_never_deliver(v):
+    """A verdict no step of the table names (VerdictFCS, an unknown value, a corrupted status
+    byte) on a frame that would otherwise be delivered ends with an error, never at a socket."""
+    gates, verr = go_gates()
+    frames = frames_for_gates()
+    buf, off, ln = pack_frames(frames, align=1)
+    _, verdicts = coracle.digest_batch(buf, off.astype(np.int64), ln.astype(np.int32), mtu=1514)
+    reached = 0
+    for f, v0 in zip(frames, verdicts):
+        if int(v0) != 0 or len(f) < 34 or f[12:14] != b"\x08\x00":
+            continue
+        ps = Stack(f[0:6], b"\0\0\0\0", 1, 1, False, 1514)
+        if recv_eth_batch_table(f, 0, ps, gates, verr)[0] != "deliver":
+            continue
+        got = recv_eth_batch_table(f, v, ps, gates, verr)
+        assert got[0] != "deliver", f"verdict {v} delivered"
+        assert got == ("err", "errUnexpectedVerdict"), got
+        reached += 1
+    assert reached > 20

@@ -103,6 +103,31 @@ def test_frames_at_buffer_start_and_tiny(engine):
     check(engine, buf, off, ln, label="start")
 
 
+@pytest.mark.parametrize("base", [4, 8, 12])
+def test_frames_base_not_16_aligned(engine, base):
+    """The frames pointer only has to be 4-byte aligned: a base at 16k + 4/8/12 (a view into a larger
+    device buffer) gives the same results, and the small-frame kernel reads 16-B chunks at absolute
+    16-B boundaries. Short frames, MTU frames and jumbo frames at every start."""
+    import framegen
+
+    frames = framegen.edge_batch(31, n_random=300)
+    buf, off, ln = pack_frames(frames, align=1)
+    dig, est = coracle.digest_batch(buf, off, ln, mtu=1514, nthreads=8)
+    dev = torch.device("cuda:0")
+    big = torch.zeros(len(buf) + 64, dtype=torch.uint8, device=dev)
+    assert big.data_ptr() % 16 == 0
+    big[base:base + len(buf)] = torch.from_numpy(buf).to(dev)
+    view = big[base:base + len(buf)]
+    assert view.data_ptr() % 16 == base
+    out, st = engine.digest_device(view, torch.from_numpy(off.astype(np.int64)).to(dev),
+                                   torch.from_numpy(ln.astype(np.int32)).to(dev), mtu=1514)
+    torch.cuda.synchronize()
+    crc, ipc, l4c = split_digests(out.cpu().numpy())
+    st = st.cpu().numpy()
+    bad = np.nonzero((crc != dig["crc32"]) | (ipc != dig["ip_csum"]) | (l4c != dig["l4_csum"]) | (st != est))[0]
+    assert bad.size == 0, f"base +{base}: {bad.size} mismatches, first at {int(bad[0])}"
+
+
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 255, 4097])
 def test_partial_tiles(engine, n):
     buf, off, ln = synth.uniform_batch(n, 1500, seed=n)

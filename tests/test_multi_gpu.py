@@ -111,6 +111,35 @@ def test_group_fault_at_chunk1_then_exact(c4):
         g.close()
 
 
+def test_group_rccl_error_aborts_communicators(c4):
+    """an RCCL error at chunk 1's gather (fs_test_group_set_fault_gather: its grouped
+    sends and receives are already enqueued) aborts the communicators before the streams are drained,
+    so the call returns instead of waiting on a transfer; the group then refuses further calls until
+    it is recreated, and a new group is bit-exact."""
+    from seqs_amd import FramesumError
+    from seqs_amd.framesum import TEST_LIB_PATH
+
+    buf, off, ln, dig, est = c4
+    devices = list(range(ndev()))
+    g = Group(devices, lib_path=TEST_LIB_PATH)
+    try:
+        shards = shards_on(devices, buf, off, ln)
+        assert g.lib.fs_test_group_set_fault_gather(g._g, 1) == 0
+        with pytest.raises(FramesumError, match="communicators were aborted"):
+            g.digest_sharded(shards, len(ln))
+        assert g.lib.fs_test_group_set_fault_gather(g._g, -1) == 0
+        with pytest.raises(FramesumError, match="aborted by an earlier error"):
+            g.digest_sharded(shards, len(ln))
+    finally:
+        g.close()
+    g = Group(devices, lib_path=TEST_LIB_PATH)
+    try:
+        words, status = g.digest_sharded(shards_on(devices, buf, off, ln), len(ln))
+        assert_equal_words(words.cpu().numpy(), status.cpu().numpy(), dig, est, "recreated group")
+    finally:
+        g.close()
+
+
 def test_group_rejects_duplicate_devices():
     from seqs_amd import FramesumError
 
