@@ -622,13 +622,21 @@ def main():
     if rank == 0 and world == 1 and args.config == "c2" and args.op == "digest" and not args.no_sub:
         # BASELINE configs[2] and [4] beside the C2 headline: the C3
         # mixed batch device-resident (same steps and warmup) and the C5 jumbo batch end to end
-        # from pinned host memory; each bounded to a few seconds
+        # from pinned host memory; the reference's 47-B benchmark frames device-resident and
+        # host-staged; the TX fill and the FCS verify; each bounded to a
+        # few seconds
         GPU.empty_cache()
         result["c3"] = sub_record_c3(args, dev)
         GPU.empty_cache()
         result["c5_host"] = sub_record_c5(args)
         GPU.empty_cache()
         result["small"] = sub_record_small(args, dev)
+        GPU.empty_cache()
+        result["fill"] = sub_record_op(args, dev, "fill")
+        GPU.empty_cache()
+        result["fcs"] = sub_record_op(args, dev, "fcs")
+        GPU.empty_cache()
+        result["small_host"] = sub_record_small_host(args)
     if world > 1 and args.config == "c2" and args.op == "digest" and not args.no_c4:
         # the C4 strong-scaled record beside the weak-scaled C2 value (same steps / warmup)
         GPU.empty_cache()
@@ -643,10 +651,12 @@ def main():
     return result
 
 
-def single_gpu_region(engine, batches, steps: int, warmup: int, min_warm: int, ns: int, dev):
+def single_gpu_region(engine, batches, steps: int, warmup: int, min_warm: int, ns: int, dev, op: str = "digest",
+                      flags: int = 3):
     """The N = 1 step loop of main() without the gather: prewarm over the streams, host spin,
     warmup steps, then K timed steps (barrier-free: one rank) closed by a polled settle and a
-    synchronize; then K back-to-back launches on one stream between HIP events. Returns
+    synchronize; then K back-to-back launches on one stream between HIP events. op: "digest"
+    (fs_digest_batch), "fill" (fs_fill_batch with `flags`) or "fcs" (fs_digest_batch_fcs). Returns
     (elapsed seconds of the K steps, average kernel ms)."""
     import torch
 
@@ -669,7 +679,7 @@ def single_gpu_region(engine, batches, steps: int, warmup: int, min_warm: int, n
         if f is None:
             fb, fo, fl = batches[i % nb]
             f = prepared[key] = engine.prepare_digest(fb, fo, fl, mtu=0, out=outs[i % nslot], status=stats[i % nslot],
-                                                      stream=s)
+                                                      stream=s, op=op, flags=flags)
         f()
 
     for i in range(max(0, min_warm - warmup)):
@@ -765,6 +775,115 @@ def sub_record_small(args, dev):
         "kernel_chosen": chosen,
         "note": "whole-job value over the same steps/warmup and streams as the headline; a latency-bound shape "
                 "(3 MB per step): frames/s, not the HBM fraction, is its figure",
+        "wall_s": round(time.perf_counter() - t_start, 2),
+    }
+
+
+def sub_record_op(args, dev, op: str):
+    """SURVEY.md §8f ranks 2 and 4 beside the RX headline, on C2's shape,
+    the same steps and warmup: "fill" = the TX checksum fill with FCS append in place
+    (fs_fill_batch FS_FILL_CSUM | FS_FCS_APPEND; stacks/port_tcp.go:162-194 fills the IPv4 and TCP
+    checksums of every frame it sends), "fcs" = the RX of wire frames that still carry their FCS
+    (fs_digest_batch_fcs). 4 resident batches of 65,536 x 1500-B frames, each with 4 spare bytes
+    after it (the FCS). Algorithmic bytes: the frame bytes read (fill: the 1500-B frames, which it
+    also rewrites in 8 bytes: the two checksum fields and the FCS; fcs: the 1504-B wire frames)."""
+    import torch
+
+    engine = GPU.engine(0)
+    t_start = time.perf_counter()
+    batches = []
+    for b in range(4):
+        buf, off, ln = with_room(*make_batch("c2", 65536, seed=501 + b))
+        tb, to, tl = torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)
+        if op == "fcs":  # wire frames: the FCS appended once, the lengths include it
+            engine.fill_device(tb, to, tl, flags=2)
+            tl = tl + 4
+        batches.append((tb, to, tl))
+    nbytes = int(batches[0][2].sum().item())
+    elapsed, k_ms = single_gpu_region(engine, batches, args.steps, args.warmup, args.min_warm, max(1, args.streams), dev,
+                                      op=op, flags=3)
+    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine.last_kernel())
+    # the results of the last launches: every frame filled / verified
+    GPU.sync()
+    engine.close()
+    del batches
+    return {
+        "workload": {"fill": "TX checksum fill + FCS append in place (fs_fill_batch FS_FILL_CSUM|FS_FCS_APPEND) of "
+                             "65536 x 1500-B TCP frames, 4 spare bytes after each",
+                     "fcs": "RX of 65536 x 1504-B wire frames (1500 B + FCS) through fs_digest_batch_fcs"}[op],
+        "value": round(nbytes * args.steps / elapsed / GIB, 3),
+        "unit": "GiB/s",
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "bytes_per_step": nbytes,
+        "kernel_avg_us": round(k_ms * 1e3, 3),
+        "frac": round(nbytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "frac_whole_job": round(nbytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+        "kernel_chosen": chosen,
+        "note": "whole-job value over the same steps/warmup and streams as the headline; frac = frame bytes read / "
+                "kernel_avg_us (HIP events around K back-to-back launches on one stream) / 8 TB/s"
+                + ("; the fill also writes 8 B per frame (checksum fields + FCS), written back as dirty lines"
+                   if op == "fill" else ""),
+        "wall_s": round(time.perf_counter() - t_start, 2),
+    }
+
+
+def sub_record_small_host(args):
+    """The reference's benchmark shape through the host-staged call the Go RecvEthBatch binding makes
+    (stacks/benchmark_test.go:12-46 sends 47-B UDP frames through RecvEth,
+    stacks/portstack.go:163): 65,536 x 47-B frames in pinned host memory, their offsets and lengths
+    pinned beside them (go/eth/digest_gpu.go stages them so), fs_digest_batch_host with the automatic
+    kernel choice (every frame <= 128 B: the small-frame kernel), results into pageable host arrays
+    (the Go caller's slices). PCIe-inclusive; the C oracle on the same frames beside it, 16 threads
+    and 1."""
+    from seqs_amd import Engine
+
+    t_start = time.perf_counter()
+    eng = Engine(0)
+    buf, off, ln = make_batch("small", 65536, seed=77)
+    n, nbytes = len(ln), int(ln.astype(np.int64).sum())
+    pin = eng.host_empty(buf.shape, np.uint8)
+    pin[:] = buf
+    poff = eng.host_empty(off.shape, np.uint64)
+    poff[:] = off
+    plen = eng.host_empty(ln.shape, np.uint32)
+    plen[:] = ln
+    from seqs_amd.framesum import DIGEST_DTYPE
+    out = np.zeros(n, dtype=DIGEST_DTYPE)
+    st = np.zeros(n, dtype=np.uint8)
+    pout = eng.host_empty((n,), DIGEST_DTYPE)
+    pst = eng.host_empty((n,), np.uint8)
+    steps, warm = max(args.steps, 100), max(args.warmup, 20)
+    res = {}
+    for name, o, s in (("pageable_results", out, st), ("pinned_results", pout, pst)):
+        for _ in range(warm):
+            eng.digest_host(pin, poff, plen, out=o, status=s)
+        gc.disable()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.digest_host(pin, poff, plen, out=o, status=s)
+        res[name] = time.perf_counter() - t0
+        gc.enable()
+    assert np.array_equal(out, pout) and np.array_equal(st, pst)
+    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(eng.last_kernel())
+    eng.close()
+    el = res["pageable_results"]
+    cpu = cpu_baseline("small", 4.0, args.cpu_threads) if args.cpu_seconds > 0 else None
+    return {
+        "workload": "65536 x 47-B UDP 'hello' frames (stacks/benchmark_test.go:12-46) host-staged through "
+                    "fs_digest_batch_host: frames + descriptors pinned, results into pageable arrays (the Go "
+                    "RecvEthBatch binding's arrangement)",
+        "value": round(nbytes * steps / el / GIB, 3),
+        "unit": "GiB/s",
+        "frames_per_s": round(n * steps / el, 1),
+        "us_per_call": round(el / steps * 1e6, 2),
+        "us_per_call_pinned_results": round(res["pinned_results"] / steps * 1e6, 2),
+        "steps": steps,
+        "warmup": warm,
+        "bytes_per_step": nbytes,
+        "transfer_bytes_per_call": {"h2d": nbytes + 12 * n, "d2h": 9 * n},
+        "kernel_chosen": chosen,
+        "cpu_baseline": cpu,
+        "note": "PCIe-inclusive (not the HBM metric); cpu_baseline: the C oracle on the same 47-B frames",
         "wall_s": round(time.perf_counter() - t_start, 2),
     }
 

@@ -119,37 +119,43 @@ func (g *GPU) SetKernel(variant int) error {
 
 // stage packs frames back to back, each at a 4-byte aligned offset, into pinned memory,
 // followed by 16 spare bytes (slack for the dword-rounded copy span; on the device the engine
-// reads the 64-byte blocks around each frame inside its own staging buffer). The
-// copies run on the host; the device reads the pinned buffer over PCIe in chunks that
-// overlap its kernels (fs_digest_batch_host).
+// reads the 64-byte blocks around each frame inside its own staging buffer). The frames'
+// offsets and lengths go into the same pinned allocation, after the frames, so that
+// fs_digest_batch_host copies them to the device straight from there (no mirror copy on the
+// host; DESIGN.md §5.3). The device reads the pinned buffer over PCIe.
 func (g *GPU) stage(frames [][]byte, spare int) ([]byte, error) {
 	n := len(frames)
-	if cap(g.offs) < n {
-		g.offs = make([]uint64, n)
-		g.lens = make([]uint32, n)
-	}
-	g.offs, g.lens = g.offs[:n], g.lens[:n]
 	total := 0
-	for i, f := range frames {
-		g.offs[i] = uint64(total)
-		g.lens[i] = uint32(len(f))
+	for _, f := range frames {
 		total += (len(f) + spare + 3) &^ 3
 	}
 	total += 16
-	if total > g.pcap {
+	desc := (total + 7) &^ 7 // the descriptors, 8-byte aligned, after the frames
+	need := desc + 12*n
+	if need > g.pcap {
 		if g.pin != nil {
 			C.fs_host_free(g.ctx, g.pin)
 			g.pin, g.pcap = nil, 0
 		}
 		var p unsafe.Pointer
-		if st := C.fs_host_alloc(g.ctx, C.uint64_t(total), &p); st != C.FS_SUCCESS {
+		if st := C.fs_host_alloc(g.ctx, C.uint64_t(need), &p); st != C.FS_SUCCESS {
 			return nil, g.lastErr()
 		}
-		g.pin, g.pcap = p, total
+		g.pin, g.pcap = p, need
 	}
-	buf := unsafe.Slice((*byte)(g.pin), total)
+	mem := unsafe.Slice((*byte)(g.pin), need)
+	g.offs, g.lens = nil, nil
+	if n > 0 {
+		g.offs = unsafe.Slice((*uint64)(unsafe.Pointer(&mem[desc])), n)
+		g.lens = unsafe.Slice((*uint32)(unsafe.Pointer(&mem[desc+8*n])), n)
+	}
+	buf := mem[:total]
+	pos := 0
 	for i, f := range frames {
-		copy(buf[g.offs[i]:], f)
+		g.offs[i] = uint64(pos)
+		g.lens[i] = uint32(len(f))
+		copy(buf[pos:], f)
+		pos += (len(f) + spare + 3) &^ 3
 	}
 	return buf, nil
 }

@@ -3,6 +3,7 @@
 // the gfx950 kernel (framesum_kernel.hip); a missing/unsupported device is an error.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -61,6 +62,10 @@ struct fs_ctx {
     hipStream_t copy_stream = nullptr, compute_stream = nullptr;
     hipStream_t copy_stream2 = nullptr;  // the odd chunks' frame copies
     hipEvent_t desc_copied = nullptr;    // the batch's descriptors are on the device
+    hipEvent_t host_done = nullptr;      // a host-staged call's last device work (polled, host_wait)
+    // a host-staged call left work in flight (it failed half-way): the next one drains the
+    // context's streams first (quiesce_host_streams); a call that returns FS_SUCCESS leaves none
+    bool host_dirty = false;
     uint8_t* d_desc = nullptr;           // the batch's offsets (8 n) then lengths (4 n)
     uint64_t cap_desc_n = 0;
     // pinned host mirrors of the descriptors and results, so every per-chunk copy is
@@ -145,12 +150,41 @@ fs_status ensure_pinned(fs_ctx* ctx, uint32_t n) {
 // Every host-staged entry point starts here: the pinned mirrors and the staging slots are free
 // only once the context's compute stream AND both copy streams are idle (a host-staged call that
 // failed half-way may have left odd-chunk copies in flight on copy_stream2 that would otherwise
-// write a slot while the next call stages into it).
+// write a slot while the next call stages into it). A call that succeeded left nothing in flight
+// (its results were waited for), so the three synchronizes (~3 us each when idle) run only after
+// a failed call.
 fs_status quiesce_host_streams(fs_ctx* ctx) {
+    if (!ctx->host_dirty) return FS_SUCCESS;
     FS_HIP(ctx, hipStreamSynchronize(ctx->compute_stream));
     FS_HIP(ctx, hipStreamSynchronize(ctx->copy_stream));
     FS_HIP(ctx, hipStreamSynchronize(ctx->copy_stream2));
+    ctx->host_dirty = false;
     return FS_SUCCESS;
+}
+
+// Wait on the host for `ev` by polling: HIP's blocking wait wakes the host about 25 us after the
+// work ends, a third of a short host-staged call. After 2 ms of polling (a long
+// batch) it falls back to the blocking wait instead of burning the core.
+hipError_t host_wait(hipEvent_t ev) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) return hipEventSynchronize(ev);
+    }
+}
+
+// Is [p, p + bytes) page-locked host memory the GPU can copy from / to asynchronously (fs_host_alloc,
+// hipHostMalloc, hipHostRegister)? Then a host-staged call copies straight from / to it instead of
+// going through the context's pinned mirror (one host memcpy less per array).
+bool is_pinned(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: not an error of the call
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
 }
 
 // One launch of the context's kernel choice.
@@ -225,6 +259,7 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->compute_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->desc_copied, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->host_done, hipEventDisableTiming);
     for (int k = 0; k < kHostSlots && e == hipSuccess; ++k) {
         e = hipEventCreateWithFlags(&ctx->slot[k].copied, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->slot[k].consumed, hipEventDisableTiming);
@@ -249,6 +284,7 @@ fs_status fs_ctx_destroy(fs_ctx* ctx) {
     if (ctx->copy_stream2) (void)hipStreamSynchronize(ctx->copy_stream2);
     if (ctx->copy_stream2) (void)hipStreamDestroy(ctx->copy_stream2);
     if (ctx->desc_copied) (void)hipEventDestroy(ctx->desc_copied);
+    if (ctx->host_done) (void)hipEventDestroy(ctx->host_done);
     (void)hipFree(ctx->d_desc);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->compute_stream) (void)hipStreamDestroy(ctx->compute_stream);
@@ -314,6 +350,61 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
     return FS_SUCCESS;
 }
 
+// A host-staged batch that fits one staging chunk (every batch of short frames): one H2D copy of
+// the frames and one of the descriptors on the two copy streams at once, one launch, the results'
+// D2H, and a polled wait. Descriptors and results go straight from / to the caller's arrays when
+// those are pinned (fs_host_alloc), through the context's pinned mirror otherwise.
+static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
+                      const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status,
+                      const framesum::plan::Scan& sc, int force) {
+    uint64_t cpy_lo, cpy_hi;
+    framesum::plan::copy_span(sc.lo, sc.hi, frames_bytes, cpy_lo, cpy_hi);
+    HostSlot& sl = ctx->slot[0];
+    fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, n);
+    if (st != FS_SUCCESS) return st;
+    const bool pin_desc = is_pinned(offsets) && is_pinned(lengths);
+    const bool pin_out = is_pinned(out) && (!status || is_pinned(status));
+    if (!pin_desc || !pin_out) {
+        st = ensure_pinned(ctx, n);
+        if (st != FS_SUCCESS) return st;
+    }
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pin);
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pin + (size_t)n * 8);
+    fs_digest* h_out = pin_out ? out : reinterpret_cast<fs_digest*>(ctx->h_pin + (size_t)n * 12);
+    uint8_t* h_st = pin_out ? status : ctx->h_pin + (size_t)n * 20;
+    const hipStream_t ks = ctx->compute_stream;
+    // the frames on one DMA queue while the descriptors go on the other
+    FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, ctx->copy_stream));
+    FS_HIP(ctx, hipEventRecord(sl.copied, ctx->copy_stream));
+    if (!pin_desc) {
+        std::memcpy(h_off, offsets, (size_t)n * 8);
+        std::memcpy(h_len, lengths, (size_t)n * 4);
+    }
+    FS_HIP(ctx, hipMemcpyAsync(sl.d_offsets, pin_desc ? offsets : h_off, (size_t)n * 8, hipMemcpyHostToDevice,
+                               ctx->copy_stream2));
+    FS_HIP(ctx, hipMemcpyAsync(sl.d_lengths, pin_desc ? lengths : h_len, (size_t)n * 4, hipMemcpyHostToDevice,
+                               ctx->copy_stream2));
+    FS_HIP(ctx, hipEventRecord(ctx->desc_copied, ctx->copy_stream2));
+    FS_HIP(ctx, hipStreamWaitEvent(ks, ctx->desc_copied, 0));
+    FS_HIP(ctx, hipStreamWaitEvent(ks, sl.copied, 0));
+    if (ctx->fault_chunk == 0) return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: injected failure (test hook)");
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
+    FS_HIP(ctx, launch(ctx, base, sl.d_offsets, sl.d_lengths, n, mtu, sl.d_out, status ? sl.d_status : nullptr, ks,
+                       framesum::FsOp::kDigest, nullptr, 0, force));
+    FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
+    sl.used = true;
+    FS_HIP(ctx, hipMemcpyAsync(h_out, sl.d_out, (size_t)n * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
+    if (status) FS_HIP(ctx, hipMemcpyAsync(h_st, sl.d_status, n, hipMemcpyDeviceToHost, ks));
+    FS_HIP(ctx, hipEventRecord(ctx->host_done, ks));
+    FS_HIP(ctx, host_wait(ctx->host_done));
+    if (!pin_out) {
+        std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
+        if (status) std::memcpy(status, h_st, n);
+    }
+    ctx->host_dirty = false;
+    return FS_SUCCESS;
+}
+
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status) {
     if (!ctx) return FS_E_INVALID;
@@ -322,14 +413,16 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     if (n > kMaxFrames) return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: n too large (at most 2^31 frames per call)");
     if (!frames || !offsets || !lengths || !out)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: null pointer");
-    uint32_t max_len = 0;
-    const uint32_t bad = framesum::plan::first_frame_out_of_range(offsets, lengths, n, frames_bytes, 0, &max_len);
-    if (bad < n)
-        return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(bad) + " ends past frames_bytes");
-    const int force = ctx->force_kernel == 0 && max_len <= kSmallAutoMaxLen ? 8 : ctx->force_kernel;
+    const framesum::plan::Scan sc = framesum::plan::scan_batch(offsets, lengths, n, frames_bytes);
+    if (sc.bad < n)
+        return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
+    const int force = ctx->force_kernel == 0 && sc.max_len <= kSmallAutoMaxLen ? 8 : ctx->force_kernel;
     FS_HIP(ctx, hipSetDevice(ctx->device));
     fs_status pst = quiesce_host_streams(ctx);
     if (pst != FS_SUCCESS) return pst;
+    ctx->host_dirty = true;  // until this call has waited for all of its work
+    if (n <= kChunkFrames && sc.hi - sc.lo <= kChunkBytes)
+        return host_single(ctx, frames, frames_bytes, offsets, lengths, n, mtu, out, status, sc, force);
     pst = ensure_pinned(ctx, n);
     if (pst != FS_SUCCESS) return pst;
     pst = ensure_desc(ctx, n);
@@ -361,7 +454,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     // chunk k's results from the pinned mirror into the caller's arrays, once they have landed
     auto deliver = [&](size_t k) -> fs_status {
         const framesum::plan::Chunk& c = chunks[k];
-        FS_HIP(ctx, hipEventSynchronize(ctx->slot[k % kHostSlots].landed));
+        FS_HIP(ctx, host_wait(ctx->slot[k % kHostSlots].landed));
         std::memcpy(out + c.c0, h_out + c.c0, (size_t)(c.c1 - c.c0) * sizeof(fs_digest));
         if (status) std::memcpy(status + c.c0, h_st + c.c0, c.c1 - c.c0);
         return FS_SUCCESS;
@@ -409,6 +502,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         if (st != FS_SUCCESS) return st;
     }
     FS_HIP(ctx, hipStreamSynchronize(ks));
+    ctx->host_dirty = false;
     return FS_SUCCESS;
 }
 
@@ -437,6 +531,7 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
     FS_HIP(ctx, hipSetDevice(ctx->device));
     fs_status pst = quiesce_host_streams(ctx);
     if (pst != FS_SUCCESS) return pst;
+    ctx->host_dirty = true;  // until this call has waited for all of its work
     pst = ensure_pinned(ctx, n);
     if (pst != FS_SUCCESS) return pst;
     uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pin);
@@ -464,6 +559,7 @@ fs_status fs_fill_batch_host(fs_ctx* ctx, uint8_t* frames, uint64_t frames_bytes
     FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
     sl.used = true;
     FS_HIP(ctx, hipStreamSynchronize(ks));
+    ctx->host_dirty = false;
     std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
     if (status) std::memcpy(status, h_st, n);
     return FS_SUCCESS;

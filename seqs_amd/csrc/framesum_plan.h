@@ -102,6 +102,38 @@ inline uint32_t first_frame_out_of_range(const uint64_t* offsets, const uint32_t
     return n;
 }
 
+// One pass over a host batch's descriptors (fs_digest_batch_host): whether every frame lies in
+// [0, frames_bytes) (overflow-safe), the longest frame, and the byte span [lo, hi) of the whole
+// batch. Branch-free in the loop (the compiler vectorizes it): the host-staged call of a batch of
+// short frames walks 65,536 descriptors per call, and two passes of a branchy loop were a sizeable
+// part of its host time. bad = the first out-of-range frame, or n.
+struct Scan {
+    uint32_t bad = 0, max_len = 0;
+    uint64_t lo = 0, hi = 0;
+};
+inline Scan scan_batch(const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint64_t frames_bytes,
+                       uint32_t extra = 0) {
+    Scan s;
+    uint64_t any_bad = 0, lo = UINT64_MAX, hi = 0;
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t o = offsets[i], need = (uint64_t)lengths[i] + extra;
+        // out of range iff o > frames_bytes or need > frames_bytes - o (no wrap: the second test
+        // only counts when the first passes)
+        const uint64_t room = frames_bytes - (o <= frames_bytes ? o : frames_bytes);
+        any_bad |= (uint64_t)(o > frames_bytes) | (uint64_t)(need > room);
+        const uint64_t e = o + lengths[i];
+        lo = o < lo ? o : lo;
+        hi = e > hi ? e : hi;
+        mx = lengths[i] > mx ? lengths[i] : mx;
+    }
+    s.bad = any_bad ? first_frame_out_of_range(offsets, lengths, n, frames_bytes, extra) : n;
+    s.max_len = mx;
+    s.lo = n ? lo : 0;
+    s.hi = hi;
+    return s;
+}
+
 struct Chunk {
     uint32_t c0, c1;          // frames [c0, c1)
     uint64_t cpy_lo, cpy_hi;  // host bytes [cpy_lo, cpy_hi) staged for them

@@ -54,24 +54,28 @@ typedef struct {
 
 static uint8_t* stage(gpu* g, const frame_list* fl, uint32_t spare, uint64_t* total_out) {
     uint64_t total = 0;
-    g->offs = realloc(g->offs, 8 * (size_t)(fl->n + 1));
-    g->lens = realloc(g->lens, 4 * (size_t)(fl->n + 1));
-    for (uint32_t i = 0; i < fl->n; ++i) {
-        g->offs[i] = total;
-        g->lens[i] = fl->len[i];
-        total += ((uint64_t)fl->len[i] + spare + 3) & ~(uint64_t)3;
-    }
+    for (uint32_t i = 0; i < fl->n; ++i) total += ((uint64_t)fl->len[i] + spare + 3) & ~(uint64_t)3;
     total += 16;
-    if (total > g->pcap) {
+    const uint64_t desc = (total + 7) & ~(uint64_t)7; /* the descriptors after the frames, pinned too */
+    const uint64_t need = desc + 12 * (uint64_t)fl->n;
+    if (need > g->pcap) {
         if (g->pin) fs_host_free(g->ctx, g->pin);
         g->pin = NULL;
         g->pcap = 0;
         void* p = NULL;
-        if (fs_host_alloc(g->ctx, total, &p) != FS_SUCCESS) return NULL;
+        if (fs_host_alloc(g->ctx, need, &p) != FS_SUCCESS) return NULL;
         g->pin = p;
-        g->pcap = total;
+        g->pcap = need;
     }
-    for (uint32_t i = 0; i < fl->n; ++i) memcpy(g->pin + g->offs[i], fl->data[i], fl->len[i]);
+    g->offs = (uint64_t*)(g->pin + desc);
+    g->lens = (uint32_t*)(g->pin + desc + 8 * (uint64_t)fl->n);
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < fl->n; ++i) {
+        g->offs[i] = pos;
+        g->lens[i] = fl->len[i];
+        memcpy(g->pin + pos, fl->data[i], fl->len[i]);
+        pos += ((uint64_t)fl->len[i] + spare + 3) & ~(uint64_t)3;
+    }
     *total_out = total;
     return g->pin;
 }

@@ -55,6 +55,17 @@ static Batch make_batch(std::mt19937_64& rng, uint32_t n, int kind) {
 static void check_chunks(const Batch& b, uint64_t chunk_bytes, uint32_t chunk_frames) {
     const uint32_t n = (uint32_t)b.len.size();
     CHECK(first_frame_out_of_range(b.off.data(), b.len.data(), n, b.bytes) == n);
+    {   // the one-pass scan of the host-staged call: in range, longest frame, byte span
+        const Scan sc = scan_batch(b.off.data(), b.len.data(), n, b.bytes);
+        uint64_t lo = UINT64_MAX, hi = 0;
+        uint32_t mx = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            lo = std::min(lo, b.off[i]);
+            hi = std::max(hi, b.off[i] + b.len[i]);
+            mx = std::max(mx, b.len[i]);
+        }
+        CHECK(sc.bad == n && sc.max_len == mx && sc.hi == hi && sc.lo == (n ? lo : 0));
+    }
     std::vector<Chunk> ch;
     host_chunks(b.off.data(), b.len.data(), n, b.bytes, chunk_bytes, chunk_frames, ch);
     uint32_t next = 0;
@@ -248,6 +259,13 @@ int main() {
         CHECK(first_frame_out_of_range(off.data(), len.data(), 2, 119) == 1);
         CHECK(first_frame_out_of_range(off.data(), len.data(), 1, 13, 4) == 0);
         CHECK(first_frame_out_of_range(off.data(), len.data(), 1, 14, 4) == 1);
+        // scan_batch reports the same first bad frame
+        CHECK(scan_batch(off.data(), len.data(), 4, 1000).bad == 2);
+        CHECK(scan_batch(off.data(), len.data(), 2, 1000).bad == 2);
+        CHECK(scan_batch(off.data(), len.data(), 2, 119).bad == 1);
+        CHECK(scan_batch(off.data(), len.data(), 1, 13, 4).bad == 0);
+        CHECK(scan_batch(off.data(), len.data(), 1, 14, 4).bad == 1);
+        CHECK(scan_batch(off.data(), len.data(), 0, 14).bad == 0);
     }
     // multi blocks: more contexts than frames, empty batches, unordered and overlapping batches
     for (int kind = 0; kind < 5; ++kind)

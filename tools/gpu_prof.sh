@@ -29,4 +29,13 @@ SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ
 TCC_HIT_sum TCC_MISS_sum
 LIST
 done
+# the TX fill with FCS append on C2: read and write bytes per launch (the
+# dirty lines its 8 written bytes per frame leave), and its kernel trace
+i=0
+for line in FETCH_SIZE WRITE_SIZE; do
+  i=$((i+1))
+  timeout -k 10 180 rocprofv3 --pmc $line --output-format csv -d "$R/gpurun_out/prof/pmc_c2fill_$i" -o run -- \
+    python3 "$R/tools/prof_driver.py" --config c2 --op fill --iters 20 > "$R/gpurun_out/prof/pmc_c2fill_$i.log" 2>&1 \
+    || { echo "PMC fill pass $i failed"; tail -5 "$R/gpurun_out/prof/pmc_c2fill_$i.log"; exit 1; }
+done
 cd "$R" && python3 tools/prof_summary.py gpurun_out/prof gpurun_out/prof/summary

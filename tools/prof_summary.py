@@ -74,7 +74,7 @@ def trace_timing(trace_csv, bench):
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     os.makedirs(dst, exist_ok=True)
-    for cfg in ("c2", "c3"):
+    for cfg in ("c2", "c3", "c2fill"):
         stats = glob.glob(os.path.join(src, cfg, "**", "*kernel_stats.csv"), recursive=True)
         if stats:
             shutil.copy(stats[0], os.path.join(dst, f"kernel_stats_{cfg}.csv"))
@@ -107,7 +107,7 @@ def main():
         cal = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "fetch_size_calibration.json")
         if "hbm_bytes_per_launch" in out and os.path.exists(cal):
             c = json.load(open(cal))
-            f = c["pattern_factor"][c["config_pattern"][cfg]]
+            f = c["pattern_factor"][c["config_pattern"].get(cfg, c["config_pattern"]["c2"])]
             out["hbm_bytes_per_launch_calibrated"] = int(round(out["hbm_bytes_per_launch"] / f))
             out["calibration_note"] = (f"divided by {f}: the doubled FETCH_SIZE of this access pattern without "
                                        "compute over its true bytes (profiles/fetch_size_calibration.json). That "
