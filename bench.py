@@ -268,7 +268,9 @@ def cpu_rate(cfg: str, seconds: float, threads: int):
     from oracle import coracle
 
     coracle.load()
-    buf, off, ln = make_batch(cfg, 4096, seed=101)
+    # 47-B frames: 262,144 per batch (12 MB), so the per-batch start of `threads` threads is not
+    # what is timed (4,096 of them are 192 KB: 16 threads ran them slower than one)
+    buf, off, ln = make_batch(cfg, 262144 if cfg == "small" else 4096, seed=101)
     nbytes = int(ln.astype(np.int64).sum())
     coracle.digest_batch(buf, off, ln, mtu=0, nthreads=threads)  # warm
     reps, t0 = 0, time.perf_counter()
@@ -285,6 +287,7 @@ def cpu_baseline(cfg: str, seconds: float, threads: int):
     """All-cores figure (the box's CPU share) with the 1-thread figure beside it."""
     threads = threads or box_cores()
     what = {"c2": "1500-B TCP", "c4": "1500-B TCP", "c5": "9000-B TCP", "small": "47-B UDP 'hello'"}.get(cfg, "mixed")
+    nfr = 262144 if cfg == "small" else 4096
     v1, r1, nbytes, e1 = cpu_rate(cfg, seconds / 2, 1)
     vn, rn, _, en = cpu_rate(cfg, seconds / 2, threads)
     return {
@@ -293,7 +296,7 @@ def cpu_baseline(cfg: str, seconds: float, threads: int):
         "cores": threads,
         "kind": "port",
         "single_core": {"value": round(v1, 4), "unit": "GiB/s", "cores": 1},
-        "sample": f"C1-style batches of 4096 {what} frames ({nbytes} B) through oracle/framesum_oracle.c "
+        "sample": f"C1-style batches of {nfr} {what} frames ({nbytes} B) through oracle/framesum_oracle.c "
                   f"(CRC791 loop -O2 -fno-tree-vectorize + zlib crc32): {rn} batches in {en:.1f} s on {threads} "
                   f"threads, {r1} in {e1:.1f} s on 1 thread; {cpu_model()}",
     }

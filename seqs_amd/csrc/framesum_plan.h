@@ -108,30 +108,50 @@ inline uint32_t first_frame_out_of_range(const uint64_t* offsets, const uint32_t
 // short frames walks 65,536 descriptors per call, and two passes of a branchy loop were a sizeable
 // part of its host time. bad = the first out-of-range frame, or n.
 struct Scan {
-    uint32_t bad = 0, max_len = 0;
-    uint64_t lo = 0, hi = 0;
+    uint32_t bad, max_len;
+    uint64_t lo, hi;
 };
-inline Scan scan_batch(const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint64_t frames_bytes,
-                       uint32_t extra = 0) {
-    Scan s;
-    uint64_t any_bad = 0, lo = UINT64_MAX, hi = 0;
+// The reductions only (min offset, max offset, max end, max length): four independent min/max
+// chains the compiler vectorizes. Every frame lies in range iff max offset <= frames_bytes and
+// max end + extra <= frames_bytes, as long as no end wraps (frames_bytes < 2^64 - 2^33: a larger
+// buffer falls back to the per-frame test).
+struct ScanCore {
+    uint64_t lo, hi_off, hi_end;
+    uint32_t max_len;
+};
+inline ScanCore scan_core(const uint64_t* offsets, const uint32_t* lengths, uint32_t n) {
+    uint64_t lo = UINT64_MAX, ho = 0, he = 0;
     uint32_t mx = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        const uint64_t o = offsets[i], need = (uint64_t)lengths[i] + extra;
-        // out of range iff o > frames_bytes or need > frames_bytes - o (no wrap: the second test
-        // only counts when the first passes)
-        const uint64_t room = frames_bytes - (o <= frames_bytes ? o : frames_bytes);
-        any_bad |= (uint64_t)(o > frames_bytes) | (uint64_t)(need > room);
-        const uint64_t e = o + lengths[i];
+        const uint64_t o = offsets[i];
+        const uint32_t l = lengths[i];
         lo = o < lo ? o : lo;
-        hi = e > hi ? e : hi;
-        mx = lengths[i] > mx ? lengths[i] : mx;
+        ho = o > ho ? o : ho;
+        he = o + l > he ? o + l : he;
+        mx = l > mx ? l : mx;
     }
-    s.bad = any_bad ? first_frame_out_of_range(offsets, lengths, n, frames_bytes, extra) : n;
-    s.max_len = mx;
-    s.lo = n ? lo : 0;
-    s.hi = hi;
+    ScanCore c;
+    c.lo = lo;
+    c.hi_off = ho;
+    c.hi_end = he;
+    c.max_len = mx;
+    return c;
+}
+inline Scan scan_from(const ScanCore& c, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
+                      uint64_t frames_bytes, uint32_t extra = 0) {
+    Scan s;
+    const bool exact = frames_bytes < UINT64_MAX - (uint64_t(1) << 33);
+    const bool in_range = exact && c.hi_off <= frames_bytes && c.hi_end <= frames_bytes &&
+                          frames_bytes - c.hi_end >= extra;
+    s.bad = (n == 0 || in_range) ? n : first_frame_out_of_range(offsets, lengths, n, frames_bytes, extra);
+    s.max_len = c.max_len;
+    s.lo = n ? c.lo : 0;
+    s.hi = c.hi_end;
     return s;
+}
+inline Scan scan_batch(const uint64_t* offsets, const uint32_t* lengths, uint32_t n, uint64_t frames_bytes,
+                       uint32_t extra = 0) {
+    return scan_from(scan_core(offsets, lengths, n), offsets, lengths, n, frames_bytes, extra);
 }
 
 struct Chunk {
