@@ -17,8 +17,7 @@ struct FsTables {
     // Region A (64 KB): 256 entry rows x 64 dword slots. Slot 8*b + c (c = 0..7) holds
     // Z_64[b][e] (one 64-byte frame-row of stream stride); the 8 copies make the kernel's
     // lookups LDS-bank-conflict-free (the 256-B entry stride lets one v_perm_b32 form the
-    // address). Slots 32..63 hold Z_704 in the mixed-length kernel (built from z704_basis), nothing in
-    // the others.
+    // address). Slots 32..63 are unused (the captured header slots do not overlap them).
     uint32_t region_a[256][64];
     uint32_t z32[4][256];      // Z_32 : lane-tree level 1 (lanes l, l+2)
     uint32_t z16[4][256];      // Z_16 : lane-tree level 2 (lanes l, l+1)
@@ -33,9 +32,6 @@ struct FsTables {
     // T[b][1 << j] of the 40 plain [4][256] tables above, in LDS-image order (piece p = 4 t + b is the
     // 1-KB piece at LDS byte 1024 p): the kernels build them in place by VALU, as region A
     uint32_t plain_basis[40][8];
-    // Z_704[b][1 << j]: the mixed-length kernel builds Z_704 in region A's unused upper halves
-    // (slots 32..63 of each entry row) from these
-    uint32_t z704_basis[4][8];
 };
 constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 10;  // the LDS image: everything before z64_basis
 static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout");

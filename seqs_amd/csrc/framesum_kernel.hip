@@ -89,7 +89,7 @@ constexpr uint32_t kLdsHdr = kLdsTables;
 static_assert(kLdsRegionA < 65536, "ds_read offset field");
 // mode B pieces (see "Tiles, pieces and passes")
 constexpr int kPieceRows = 12;
-
+constexpr int kPieceDwords = kPieceRows * kRowDwords;  // 192 dwords = 768 bytes
 constexpr int kMaxFullPasses = 6;
 constexpr uint32_t kWaveScratchBytes = 16u * kFramesPerTile + 8u * kFramesPerTile +
                                        8u * (kFramesPerTile + kFramesPerTile * kMaxFullPasses);
@@ -212,6 +212,35 @@ __device__ __forceinline__ void lean_row(const char* lds, const LaneKeys& k, u32
     cs = sad16(v.y, cs);
     cs = sad16(v.z, cs);
     cs = sad16(v.w, cs);
+}
+
+// A masked row: the chunk was loaded from frame dword p (= rel unless clamped up, see
+// load_pos); realign it to [rel, rel+4), zero the dwords before the frame, mask the head and
+// tail bytes and apply the CRC init.
+// nd: frame dwords (0 = nothing to stream); sa: S & 3; tail_mask: bytes of dword nd-1 inside
+// the frame. The head mask (bytes of dword 0 inside the frame) is also the CRC init's part in
+// dword 0; its complement is the init's part in dword 1.
+template <uint32_t kRegion = kLdsRegionA>
+__device__ __forceinline__ void masked_row(const char* lds, const LaneKeys& k, u32x4 u, int rel, int p, int nd,
+                                           uint32_t sa, uint32_t tail_mask, uint32_t (&A)[4], uint32_t& cs) {
+    const uint32_t head_mask = 0xffffffffu << (8u * sa);
+    const int sh = p - rel;  // > 0 only for a clamped chunk; then every dword below p lies before the frame
+    uint32_t v[4];
+    v[0] = u.x;
+    v[1] = (sh == 0) ? u.y : u.x;
+    v[2] = (sh == 0) ? u.z : (sh == 1) ? u.y : u.x;
+    v[3] = (sh == 0) ? u.w : (sh == 1) ? u.z : (sh == 2) ? u.y : u.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int x = rel + j;
+        uint32_t d = (x >= 0) ? v[j] : 0u;
+        uint32_t c = 0u;
+        if (x == 0) { d &= head_mask; c = head_mask; }
+        if (x == 1) c = ~head_mask;
+        if (x == nd - 1) d &= tail_mask;
+        A[j] = zrep<kRegion>(lds, A[j], k, d ^ c);
+        cs = sad16(d, cs);
+    }
 }
 
 // Block-aligned rows (digest_kernel_a<kOps, true>): a chunk is always loaded where it lies (or,
@@ -590,31 +619,20 @@ __device__ __forceinline__ void finish_frame(const char* lds, const Parsed& P, u
 }
 
 // ---------------------------------------------------------------------------------------
-// Tiles, pieces and passes (the mixed-length kernel, digest_kernel_ab).
+// Tiles, pieces and passes.
 //
-// Every frame is read as the 64-B blocks that hold it (block-aligned rows, as the one-pass
-// kernel's): a frame of nd stream dwords whose dword 0 sits at absolute block phase ph spans
-// B = (ph + nd + e) / 16 blocks, e = the junk dwords after its end in its last block.
-// A tile's 16 frames run in PASSES of lockstep rows. MODE A (one pass): every group streams its
-// whole frame. MODE B, for tiles whose lengths differ widely: a frame is cut into a HEAD piece of
-// its first hb blocks (2 <= hb <= 13; hb = B when B <= 13) and npc - 1 FULL pieces of 12 blocks
-// (kPieceRows, 768 B) after it; pass 0 streams every group's head piece, passes 1.. the tile's
-// F full pieces, 16 per pass (full piece q -> group q mod 16 of pass 1 + q / 16).
-// Pass 0 is START-anchored: row r is block r of every group's piece, so the frame starts (the
-// masked head: the bytes before the frame in its first block, the CRC init on frame dwords 0
-// and 1) all lie in rows 0 and 1, and a piece that ends before the pass's last row leaves its
-// streams untouched from its last row on (a tail check, much cheaper than a masked row; its
-// loads past the piece reload the piece's last block). Rows past the longest piece are
-// skipped, so the pass has exactly max(hb) rows. A full piece is 12 whole blocks: lean rows,
-// the last one tail-checked (a frame's last piece ends at its last dword).
-// Each pass ends with the one-pass kernel's junk-free 16-stream combine (combine_al) of every
-// group's piece -- its streams shifted to the piece's last dword: e junk dwords before the block
-// end for a frame's last piece, none otherwise -- into one register value Y and a checksum
-// partial, parked in a per-wave LDS slot. A frame's CRC register is then the Horner fold
-// C = Z(C) ^ Y over its pieces: Z = Z768 between pieces that end on a block boundary, and
-// Z_(768 - 4e) = Z704 . Z_(64 - 4e) into the last one (Z704 lives in region A's unused upper
-// halves). Every pass runs the same row loop; the next pass's first rows are prefetched before
-// the current pass's combine.
+// A tile's 16 frames run in PASSES of lockstep rows. MODE A (one pass): every group streams
+// its whole frame, rows end-anchored at the pass end -- the lean choice when the frames have
+// similar lengths. MODE B, for tiles whose lengths differ widely: a frame of nd stream dwords
+// is cut into a HEAD piece of nd0 = nd - 192 (npc - 1) dwords (2 <= nd0 <= 193) and npc - 1
+// FULL pieces of 192 dwords (12 rows, kPieceRows) that follow it; pass 0 streams every
+// group's head piece exactly as mode A streams whole frames; passes 1.. stream the tile's F
+// full pieces, 16 per pass (full piece q -> group q mod 16 of pass 1 + q / 16), all lean.
+// Each pass ends with the 16-stream combine of every group's piece into one register value
+// Y and a checksum partial, parked in a per-wave LDS slot; a frame's CRC register is then
+// the Horner fold C = Z768(C) ^ Y over its pieces (a piece's value is its contribution as
+// if the frame ended with it; Z768 shifts it past one full piece). Every pass runs the same
+// row loop; the next pass's first rows are prefetched before the current pass's combine.
 
 // The group's own frame (parse and finish). Every lane describes its GROUP's frame (the 4
 // lanes of a group load the same descriptor; the group's lane 0 parses, finishes and stores).
@@ -639,36 +657,18 @@ struct Tile {
     }
 };
 
-// Block geometry of a frame (offset S, length len): the absolute 64-B block phase ph (in dwords)
-// of its dword 0, its stream dwords nd (0 under 4 bytes), the junk dwords e after its end in its
-// last block, its blocks B, its pieces npc and its head piece's blocks hb.
-struct Geo {
-    uint32_t ph;
-    int nd, e, B, npc, hb;
-};
-__device__ __forceinline__ Geo frame_geo(const uint8_t* frames, uint64_t S, uint32_t len) {
-    Geo g;
-    g.ph = (uint32_t)((reinterpret_cast<uint64_t>(frames) >> 2) + (S >> 2)) & 15u;
-    g.nd = len >= 4u ? (int)((((uint32_t)S & 3u) + len + 3u) >> 2) : 0;
-    g.e = (16 - (int)((g.ph + (uint32_t)g.nd) & 15u)) & 15;
-    g.B = g.nd > 0 ? (int)((g.ph + (uint32_t)(g.nd + g.e)) >> 4) : 0;
-    g.npc = g.B > 1 ? (g.B - 1 + kPieceRows - 1) / kPieceRows : 1;
-    g.hb = g.B - kPieceRows * (g.npc - 1);
-    return g;
-}
+__device__ __forceinline__ int pieces_of(int nd) { return nd <= 1 ? 1 : (nd - 1 + kPieceDwords - 1) / kPieceDwords; }
 
-// The rows one pass streams, per group.
+// The rows one pass streams.
 struct Unit {
-    const uint32_t* gfb;  // frame dword 0 of the piece's frame (a longest piece's frame for an empty group)
-    int rel0;    // frame dword of this lane's chunk in row 0
-    int relmax;  // the lane's chunk of the piece's last block: loads of rows past the piece reload it
-    int ndp;     // frame dwords at or past this one are not streamed (the frame end for its last piece)
-    uint32_t tmask;  // bytes of dword ndp - 1 inside the frame (all of them unless the piece ends the frame)
-    int esh;     // junk dwords after the piece's last dword in its last block (e for a frame's last piece)
-    int P;       // wave-uniform: rows of the pass (0 = no rows)
-    int H;       // wave-uniform: leading rows that take the masked path (frame dwords 0 and 1)
-    int Lt;      // wave-uniform: the first row that holds some piece's last block (tail-checked from there)
-    uint32_t info;  // full passes: bit 31 valid piece, bits 0-15 its slot
+    const uint32_t* gfb;  // frame dword 0 of the lane's rows (a longest frame's for an empty group)
+    int rel0;   // frame dword of this lane's chunk in row 0
+    int lo;     // lowest frame dword a clamped row load may start at
+    int P;      // wave-uniform: rows (a multiple of kPrefetch; 0 = no rows)
+    int H;      // wave-uniform: leading rows that take the masked path
+    // mode B: bit 31 valid piece, bit 30 the frame's last piece (its last dword carries the
+    // dword-rounding junk), bits 28-29 the frame's end byte in its last dword, bits 0-15 slot
+    uint32_t info;
 };
 
 __device__ __forceinline__ void tile_descriptors(uint32_t tile, uint32_t grp, uint32_t n,
@@ -720,17 +720,55 @@ struct WaveScratch {
     uint32_t slots;  // [16 + 16 * kMaxFullPasses] x {Y, csum}
 };
 
+// Pass-0 rows over `ndp` stream dwords per group (whole frames in mode A, head pieces in mode B).
+__device__ __forceinline__ void pass0_unit(Unit& U, const Tile& T, int ndp, uint32_t gl,
+                                           const uint8_t* __restrict__ frames) {
+    const int rows0 = (ndp + kRowDwords - 1) / kRowDwords;
+    const int R0 = group_max(rows0);
+    U.P = (R0 + kPrefetch - 1) / kPrefetch * kPrefetch;
+    uint64_t ld_sdw = T.sdw();
+    int ld_nd = ndp;
+    {
+        const uint64_t ball = __ballot(rows0 == R0);  // never 0: some lane holds the maximum
+        const int src = (int)__builtin_ctzll(ball);
+        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ld_sdw, src);
+        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ld_sdw >> 32), src);
+        const int s_nd = __builtin_amdgcn_readlane(ndp, src);
+        if (ndp == 0) {
+            ld_sdw = ((uint64_t)s_hi << 32) | s_lo;
+            ld_nd = s_nd;
+        }
+    }
+    U.gfb = reinterpret_cast<const uint32_t*>(frames + (ld_sdw << 2));
+    U.rel0 = ld_nd - kRowDwords * U.P + 4 * (int)gl;
+    // Loads of rows that start before the frame are clamped to the frame's first chunk (its last
+    // chunk for frames under 4 dwords), so lanes idling through a tile's longest frame re-read
+    // one cached line instead of fetching the bytes that precede their frame; a chunk that
+    // straddles the frame start is loaded where it lies unless that is below frames[0].
+    U.lo = max(ld_sdw > (1u << 24) ? -(1 << 24) : -(int)ld_sdw, min(0, ld_nd - 4));
+    // Masked rows: those holding, for some lane, a frame dword < 2 (head bytes, CRC init) or a
+    // dword before the frame. The group's lane 0 has the lowest rel: row r is lean for the
+    // group once ndp - 16 P + 16 r >= 2.
+    const int need = 2 - (ndp - kRowDwords * U.P);
+    const int h = (ndp > 0 && need > 0) ? (need + kRowDwords - 1) / kRowDwords : 0;
+    U.H = min(group_max(h), U.P);
+    U.info = 0u;
+}
+
 __device__ __forceinline__ void tile_geometry(Tile& T, Unit& U, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t n,
                                               uint64_t S, uint32_t len, const uint8_t* __restrict__ frames,
                                               char* lds, const WaveScratch& ws, uint32_t fpt) {
     T.len = (grp < fpt && tile * fpt + grp < n) ? len : 0u;
     T.S = S;
-    const Geo g = frame_geo(frames, S, T.len);
+    const int nd = T.nd();
+    const int rows = (nd + kRowDwords - 1) / kRowDwords;
+    const int RA = (group_max(rows) + kPrefetch - 1) / kPrefetch * kPrefetch;
     // mode B: pass 0 over the head pieces, then ceil(F / 16) full-piece passes of 12 rows, each
     // about 2 rows' worth of combine; taken when that beats one pass over the longest frame
-    const int RA = group_max(g.B);
-    const int P0B = group_max(g.hb);
-    const int F = group_sum(g.npc - 1);
+    const int npc = nd > 0 ? pieces_of(nd) : 1;
+    const int nd0 = nd - kPieceDwords * (npc - 1);
+    const int P0B = (group_max((nd0 + kRowDwords - 1) / kRowDwords) + kPrefetch - 1) / kPrefetch * kPrefetch;
+    const int F = group_sum(npc - 1);
     const int fullp = (F + kFramesPerTile - 1) / kFramesPerTile;
     const bool modeB = F > 0 && fullp <= kMaxFullPasses && P0B + (kPieceRows + 2) * fullp < RA;
     T.F = modeB ? F : 0;
@@ -739,7 +777,7 @@ __device__ __forceinline__ void tile_geometry(Tile& T, Unit& U, uint32_t tile, u
         // frame table, full-piece counts and their inclusive prefix (same wave: LDS in order)
         if (gl == 0u) {
             *reinterpret_cast<u32x4*>(lds + ws.ftab + 16u * grp) = u32x4{(uint32_t)S, (uint32_t)(S >> 32), T.len, 0u};
-            *reinterpret_cast<uint32_t*>(lds + ws.dpc + 4u * grp) = (uint32_t)(g.npc - 1);
+            *reinterpret_cast<uint32_t*>(lds + ws.dpc + 4u * grp) = (uint32_t)(npc - 1);
         }
         int e = 0;
 #pragma unroll
@@ -750,37 +788,7 @@ __device__ __forceinline__ void tile_geometry(Tile& T, Unit& U, uint32_t tile, u
         }
         if (gl == 0u) *reinterpret_cast<uint32_t*>(lds + ws.epre + 4u * grp) = (uint32_t)e;
     }
-    // pass 0: every group's head piece (mode B) or whole frame (mode A), start-anchored
-    const int pb = modeB ? g.hb : g.B;      // blocks of the group's pass-0 piece (0: empty group)
-    const bool ends = !modeB || g.npc == 1;  // the piece ends the frame
-    U.P = modeB ? P0B : RA;
-    uint64_t ld_sdw = T.sdw();
-    int ld_pb = pb;
-    uint32_t ld_ph = g.ph;
-    {   // an empty group addresses the rows of a longest piece of the tile (valid loads, ignored)
-        const uint64_t ball = __ballot(pb == U.P);  // never 0: some lane holds the maximum
-        const int src = (int)__builtin_ctzll(ball);
-        const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ld_sdw, src);
-        const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ld_sdw >> 32), src);
-        const int s_pb = __builtin_amdgcn_readlane(pb, src);
-        const uint32_t s_ph = (uint32_t)__builtin_amdgcn_readlane((int)ld_ph, src);
-        if (pb == 0) {
-            ld_sdw = ((uint64_t)s_hi << 32) | s_lo;
-            ld_pb = s_pb;
-            ld_ph = s_ph;
-        }
-    }
-    U.gfb = reinterpret_cast<const uint32_t*>(frames + (ld_sdw << 2));
-    U.rel0 = 4 * (int)gl - (int)ld_ph;
-    U.relmax = U.rel0 + kRowDwords * max(ld_pb - 1, 0);
-    U.ndp = pb == 0 ? -(1 << 20) : ends ? g.nd : kRowDwords * pb - (int)g.ph;
-    U.tmask = ends ? T.tail_mask() : 0xffffffffu;
-    U.esh = ends ? g.e : 0;
-    // masked rows: every piece's block 0 (the bytes before the frame, the CRC init on dword 0), and
-    // block 1 when it starts with some frame's dword 1 (ph = 15)
-    U.H = U.P == 0 ? 0 : __ballot(pb > 0 && g.ph == 15u && g.nd > 1) ? min(2, U.P) : 1;
-    U.Lt = -group_max(pb > 0 ? -pb : -(1 << 20)) - 1;  // min pb - 1
-    U.info = 0u;
+    pass0_unit(U, T, modeB ? nd0 : nd, gl, frames);
 }
 
 // The full piece a group streams in pass p >= 1 (mode B): q = 16 (p - 1) + group; groups past
@@ -804,35 +812,34 @@ __device__ __forceinline__ void full_piece_unit(Unit& U, const char* lds, const 
     }
     const u32x4 fr = *reinterpret_cast<const u32x4*>(lds + ws.ftab + 16u * (uint32_t)i);
     const uint64_t S = ((uint64_t)fr.y << 32) | fr.x;
-    const uint32_t len = fr.z;
-    const Geo g = frame_geo(frames, S, len);
-    const int k = q - ebefore + 1;  // 1 .. npc - 1
-    const bool last = k == g.npc - 1;
+    const uint32_t len = fr.z, sa = (uint32_t)S & 3u;
+    const int nd = (int)((sa + len + 3u) >> 2);
+    const int npc = pieces_of(nd);
+    const int k = q - ebefore + 1;                 // 1 .. npc - 1
     U.gfb = reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2));
-    U.rel0 = kRowDwords * (g.hb + kPieceRows * (k - 1)) - (int)g.ph + 4 * (int)gl;
-    U.relmax = U.rel0 + kRowDwords * (kPieceRows - 1);
-    U.ndp = last ? g.nd : (1 << 30);
-    const uint32_t te = (((uint32_t)S & 3u) + len) & 3u;
-    U.tmask = last && te ? ((1u << (8u * te)) - 1u) : 0xffffffffu;
-    U.esh = last ? g.e : 0;
+    U.rel0 = nd - kPieceDwords * (npc - k) + 4 * (int)gl;  // the piece's first dword + the lane's chunk
+    U.lo = 0;
     U.P = kPieceRows;
     U.H = 0;
-    U.Lt = kPieceRows - 1;
-    U.info = (q0 < F ? 0x80000000u : 0u) | (uint32_t)(kFramesPerTile + q);
+    U.info = (q0 < F ? 0x80000000u : 0u) | (k == npc - 1 ? 0x40000000u : 0u) | (((sa + len) & 3u) << 28) |
+             (uint32_t)(kFramesPerTile + q);
 }
 
-// Would the tile run better in mode B? (tile_geometry's decision, for the one-pass kernel's
-// report; B = the group's frame's blocks, 0 for an empty group)
-__device__ __forceinline__ bool mode_b_worthy(int B) {
-    const int rmax = group_max(B);
-    // a tile whose frames differ by under 4 blocks (256 B) has nothing for pieces to fill: the
+// Would the tile run better in mode B? (the decision of tile_geometry, for the mode-A-only
+// kernel's report)
+__device__ __forceinline__ bool mode_b_worthy(int nd) {
+    const int rows = (nd + kRowDwords - 1) / kRowDwords;
+    const int rmax = group_max(rows);
+    // a tile whose frames differ by under 4 rows (256 B) has nothing for pieces to fill: the
     // common case of uniform batches skips the piece arithmetic (it only steers the choice)
-    if (rmax + group_max(-B) < 4) return false;
-    const int npc = B > 1 ? (B - 1 + kPieceRows - 1) / kPieceRows : 1;
-    const int P0B = group_max(B - kPieceRows * (npc - 1));
+    if (rmax + group_max(-rows) < 4) return false;
+    const int RA = (rmax + kPrefetch - 1) / kPrefetch * kPrefetch;
+    const int npc = nd > 0 ? pieces_of(nd) : 1;
+    const int nd0 = nd - kPieceDwords * (npc - 1);
+    const int P0B = (group_max((nd0 + kRowDwords - 1) / kRowDwords) + kPrefetch - 1) / kPrefetch * kPrefetch;
     const int F = group_sum(npc - 1);
     const int fullp = (F + kFramesPerTile - 1) / kFramesPerTile;
-    return F > 0 && fullp <= kMaxFullPasses && P0B + (kPieceRows + 2) * fullp < rmax;
+    return F > 0 && fullp <= kMaxFullPasses && P0B + (kPieceRows + 2) * fullp < RA;
 }
 
 // ---- the mode-A-only kernel's tile state: the group's own frame and its single pass
@@ -853,8 +860,6 @@ struct TileA {
     __device__ __forceinline__ uint32_t sa() const { return (uint32_t)S & 3u; }
     // block-aligned rows: dwords past the frame end in its last row (the row ends on a 64-B block)
     __device__ __forceinline__ int ealign() const { return (16 - (int)((ph + (uint32_t)nd()) & 15u)) & 15; }
-    // the 64-B blocks that hold the frame's stream dwords (0 for an empty group)
-    __device__ __forceinline__ int blocks() const { return nd() > 0 ? (int)((ph + (uint32_t)(nd() + ealign())) >> 4) : 0; }
     __device__ __forceinline__ uint64_t sdw() const { return S >> 2; }
     // dwords the frame touches (incl. frames under 4 bytes)
     __device__ __forceinline__ int ndall() const { return (int)((sa() + len + 3u) >> 2); }
@@ -926,18 +931,22 @@ __device__ __forceinline__ void tile_geometry_a(TileA& T, uint32_t tile, uint32_
     if (!kDeferTail) tile_geometry_a_tail<kCapBlocks>(T);
 }
 
+// Frame dword at which a masked row's chunk is loaded: where it lies, unless it starts
+// before the frame's first chunk (then the frame's first chunk: its dwords are all masked
+// or realigned) or below frames[0].
+__device__ __forceinline__ int load_pos(int rel, int lo) { return rel <= -4 ? lo : max(rel, lo); }
+
 __device__ __forceinline__ u32x4 load_row(const uint32_t* fb, int pos) {
     return *reinterpret_cast<const u32x4_a4*>(fb + pos);
 }
 
-// Row r of a pass (the mixed-length kernel): the lane's chunk of the piece's block r, or of its last
-// block for a row past the piece.
-__device__ __forceinline__ u32x4 unit_row(const Unit& U, int r) { return load_row(U.gfb, min(U.rel0 + kRowDwords * r, U.relmax)); }
-
 __device__ __forceinline__ void prefetch_unit(const Unit& U, u32x4 (&pf)[kPrefetch]) {
     if (U.P > 0) {  // a tile of frames all under 4 bytes loads no rows (they could lie past the buffer)
 #pragma unroll
-        for (int i = 0; i < kPrefetch; ++i) pf[i] = unit_row(U, i);
+        for (int i = 0; i < kPrefetch; ++i) {
+            const int rel = U.rel0 + kRowDwords * i;
+            pf[i] = load_row(U.gfb, i < U.H ? load_pos(rel, U.lo) : rel);
+        }
     }
 }
 
@@ -956,13 +965,6 @@ __device__ __forceinline__ uint64_t sgpr_addr(const void* p) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
 }
-// Z_704 (the mixed-length kernel's fold into a frame's last piece) in region A's unused upper
-// halves: byte table b, entry e at e * 256 + 128 + 4 (8 b + (e & 7)) -- a byte table's random
-// entries spread over 8 banks.
-__device__ __forceinline__ uint32_t z704_at(uint32_t b, uint32_t e) {
-    return kLdsRegionA + (e << 8) + 128u + 4u * (8u * b + (e & 7u));
-}
-template <bool kZ704 = false>
 __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs, char* lds) {
     typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
     const uint32_t t = threadIdx.x;
@@ -1002,17 +1004,6 @@ __device__ __forceinline__ void build_region_a(const FsTables* __restrict__ tabs
     piece(pb0, w);
     piece(pb1, w + 16u);
     if (w + 32u < 40u) piece(pb2, w + 32u);
-    if (kZ704 && w < 4u) {  // Z_704's byte table w: lane l the entries 4l .. 4l + 3
-        const uint32_t* zb = tabs->z704_basis[w];
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t j = 2; j < 8; ++j) x ^= zb[j] & (0u - ((lane >> (j - 2u)) & 1u));
-        const uint32_t x1 = x ^ zb[0];
-        *reinterpret_cast<uint32_t*>(lds + z704_at(w, 4u * lane)) = x;
-        *reinterpret_cast<uint32_t*>(lds + z704_at(w, 4u * lane + 1u)) = x1;
-        *reinterpret_cast<uint32_t*>(lds + z704_at(w, 4u * lane + 2u)) = x ^ zb[1];
-        *reinterpret_cast<uint32_t*>(lds + z704_at(w, 4u * lane + 3u)) = x1 ^ zb[1];
-    }
 }
 // LDS-DMA by inline asm: invisible to hipcc's vmcnt model (the builtin makes it drain later
 // LDS reads with vmcnt(0)); unknown VMEM ops only make the compiler's own counted waits
@@ -1092,6 +1083,26 @@ __device__ __forceinline__ void tables_landed(bool first, bool rows, bool x4) {
     else __builtin_amdgcn_s_waitcnt(0x0070);
 }
 
+// 16-stream combine of a group's piece: U_l = Z12(A0) ^ Z8(A1) ^ Z4(A2) ^ A3 per lane (minus the
+// junk the piece's last dword may carry, lane 3), Y = xor_l Z_16(3-l)(U_l) over the group by
+// DPP; the checksum partial folded mod 65535 (every partial < 2^18) and summed over the group.
+__device__ __forceinline__ void combine_piece(const char* lds, uint32_t gl, const uint32_t (&A)[4], uint32_t cs,
+                                              uint32_t junk, uint32_t& Y, uint32_t& csum) {
+    const uint32_t U =
+        zplain(lds, A[0], kLdsZ12) ^ zplain(lds, A[1], kLdsZ8) ^ zplain(lds, A[2], kLdsZfin) ^ A[3] ^ junk;
+    cs -= sad16(junk, 0u);
+    const uint32_t ybase = (gl == 0u) ? kLdsZ48 : (gl == 1u) ? kLdsZ32 : kLdsZ16;
+    uint32_t y = zplain(lds, U, ybase);
+    if (gl == 3u) y = U;
+    y ^= dpp_quad<kQuadXor1>(y);
+    y ^= dpp_quad<kQuadXor2>(y);
+    cs = (cs & 0xffffu) + (cs >> 16);
+    cs += dpp_quad<kQuadXor1>(cs);
+    cs += dpp_quad<kQuadXor2>(cs);
+    Y = y;
+    csum = cs;
+}
+
 // The one-pass kernel's LDS layout: one 16-wave workgroup per CU (region A and the plain tables
 // built in place), 3-block captured header slots per wave.
 struct LayA1 : LayoutA {
@@ -1105,52 +1116,6 @@ struct LayA1 : LayoutA {
         return a ? y : v;
     }
 };
-
-// The junk-free 16-stream combine of block-aligned rows. Stream j of lane gl (row
-// position 4 gl + j) is shifted by its distance in dwords to the piece's last dword, at position
-// q = 15 - esh of its last row: s = (K - j) mod 16 with K = (q - 4 gl) mod 16 = 4 a + C (the
-// streams past q skipped the last row); then xor over the group's 4 lanes. Streams j <= C need
-// Z_(16 a) Z_(4 (C - j)), the others Z_(16 ((a - 1) & 3)) Z_(4 (4 + C - j)). Sorted by their Z4
-// class c (B_c = A_((C - c) & 3): the registers reversed, then rotated by C), that is one round of
-// Z4 / Z8 / Z12 with a fixed table per register and one round of Z_(16 a) per class: 5 lookups in
-// 2 dependent rounds (tests/kernel_model.py). The checksum partial of each lane is folded mod 65535
-// (the finish only needs the total mod 65535; every partial stays < 2^18) and summed over the group.
-__device__ __forceinline__ void combine_al(const char* lds, uint32_t gl, const uint32_t (&A)[4], uint32_t& cs,
-                                           int esh, uint32_t& Y) {
-    const uint32_t K = (uint32_t)(15 - esh - 4 * (int)gl) & 15u;
-    const uint32_t a = K >> 2, C = K & 3u;
-    const bool r1 = (C & 1u) != 0u, r2 = (C & 2u) != 0u;
-    // reversed: (A0, A3, A2, A1); rotated by 1 then by 2 where C has those bits
-    const uint32_t x0 = r1 ? A[1] : A[0], x1 = r1 ? A[0] : A[3], x2 = r1 ? A[3] : A[2], x3 = r1 ? A[2] : A[1];
-    const uint32_t b0 = r2 ? x2 : x0, b1 = r2 ? x3 : x1, b2 = r2 ? x0 : x2, b3 = r2 ? x1 : x3;
-    const uint32_t t1 = zplain(lds, b1, kLdsZfin);  // Z4
-    const uint32_t t2 = zplain(lds, b2, kLdsZ8);
-    const uint32_t t3 = zplain(lds, b3, kLdsZ12);
-    const uint32_t v1 = b0 ^ (C >= 1u ? t1 : 0u) ^ (C >= 2u ? t2 : 0u) ^ (C == 3u ? t3 : 0u);
-    const uint32_t v2 = xor3(b0 ^ t1, t2, t3) ^ v1;
-    uint32_t y = LayA1::z16a(lds, v1, a) ^ LayA1::z16a(lds, v2, (a - 1u) & 3u);
-    y ^= dpp_quad<kQuadXor1>(y);
-    y ^= dpp_quad<kQuadXor2>(y);
-    Y = y;
-    cs = (cs & 0xffffu) + (cs >> 16);
-    cs += dpp_quad<kQuadXor1>(cs);
-    cs += dpp_quad<kQuadXor2>(cs);
-}
-
-// The mixed-length kernel's fold into a frame's last piece: Z_(768 - 4e)(v) = Z704 . Z_(64 - 4e)
-// for e = 1..15 (Z768 for e = 0).
-__device__ __forceinline__ uint32_t z704(const char* lds, uint32_t v) {
-    return lds32(lds, z704_at(0u, v & 0xffu)) ^ lds32(lds, z704_at(1u, (v >> 8) & 0xffu)) ^
-           lds32(lds, z704_at(2u, (v >> 16) & 0xffu)) ^ lds32(lds, z704_at(3u, v >> 24));
-}
-__device__ __forceinline__ uint32_t z_last_piece(const char* lds, uint32_t v, int e) {
-    if (e == 0) return zplain(lds, v, kLdsZ768);
-    const uint32_t sh = 64u - 4u * (uint32_t)e;  // 4 .. 60 = 16 a + 4 c
-    const uint32_t c = (sh >> 2) & 3u, a = sh >> 4;
-    if (c) v = zplain(lds, v, c == 1u ? kLdsZfin : c == 2u ? kLdsZ8 : kLdsZ12);
-    if (a) v = zplain(lds, v, a == 1u ? kLdsZ16 : a == 2u ? kLdsZ32 : kLdsZ48);
-    return z704(lds, v);
-}
 
 // `report` = the host-mapped report word's address in bits 0..47, the launch id in bits 48..63
 // (one kernel argument, loaded where it is used: nothing of it stays live through the tile loop).
@@ -1258,7 +1223,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         for (int i = 0; i < kPfA; ++i) pf[i] = load_row(T.gfb, lpos(T.rel0 + kRowDwords * i, T.lo));
     }
     if (first) tile_geometry_a_tail<Lay::kCapBlocks>(T);
-    if (first && report && mode_b_worthy(T.blocks()) && lane == 0u) post_report(report);
+    if (first && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
     if (first) tile_header(T);
     FS_STAMP(13);
     FS_STAMP(9);
@@ -1373,11 +1338,38 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         }
         FS_STAMP(2);
 
-        // ---- combine the 16 streams of each frame (combine_al, the frame's last row: e junk dwords).
+        // ---- combine the 16 streams of each frame. Stream j of lane gl (row position 4 gl + j)
+        // is shifted by its distance in dwords to the frame's last dword, at position
+        // q = 15 - ealign() of the last row: s = (K - j) mod 16 with K = (q - 4 gl) mod 16 = 4 a + C
+        // (the streams past q skipped the last row); then xor over the group's 4 lanes.
+        // Streams j <= C need Z_(16 a) Z_(4 (C - j)), the others Z_(16 ((a - 1) & 3)) Z_(4 (4 + C - j)).
+        // Sorted by their Z4 class c (B_c = A_((C - c) & 3): the registers reversed, then rotated
+        // by C), that is one round of Z4 / Z8 / Z12 with a fixed table per register and one round
+        // of Z_(16 a) per class: 5 lookups in 2 dependent rounds (tests/kernel_model.py).
         // The parked parse, read by every lane now: its LDS round trip overlaps the combine's.
         const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
+        const uint32_t K = (uint32_t)(15 - T.ealign() - 4 * (int)gl) & 15u;
+        const uint32_t a = K >> 2, C = K & 3u;
         uint32_t Y;
-        combine_al(lds, gl, A, cs, T.ealign(), Y);
+        {
+            const bool r1 = (C & 1u) != 0u, r2 = (C & 2u) != 0u;
+            // reversed: (A0, A3, A2, A1); rotated by 1 then by 2 where C has those bits
+            const uint32_t x0 = r1 ? A[1] : A[0], x1 = r1 ? A[0] : A[3], x2 = r1 ? A[3] : A[2], x3 = r1 ? A[2] : A[1];
+            const uint32_t b0 = r2 ? x2 : x0, b1 = r2 ? x3 : x1, b2 = r2 ? x0 : x2, b3 = r2 ? x1 : x3;
+            const uint32_t t1 = zplain(lds, b1, kLdsZfin);  // Z4
+            const uint32_t t2 = zplain(lds, b2, kLdsZ8);
+            const uint32_t t3 = zplain(lds, b3, kLdsZ12);
+            const uint32_t v1 = b0 ^ (C >= 1u ? t1 : 0u) ^ (C >= 2u ? t2 : 0u) ^ (C == 3u ? t3 : 0u);
+            const uint32_t v2 = xor3(b0 ^ t1, t2, t3) ^ v1;
+            Y = Lay::z16a(lds, v1, a) ^ Lay::z16a(lds, v2, (a - 1u) & 3u);
+        }
+        Y ^= dpp_quad<kQuadXor1>(Y);
+        Y ^= dpp_quad<kQuadXor2>(Y);
+        // checksum over the 4 lanes of the group, each lane first folded mod 65535 (the finish
+        // only needs the total mod 65535; the fold keeps every partial < 2^18)
+        cs = (cs & 0xffffu) + (cs >> 16);
+        cs += dpp_quad<kQuadXor1>(cs);
+        cs += dpp_quad<kQuadXor2>(cs);
         FS_STAMP(3);
         // ---- the group's lane 0: finish and store (its frame's parse comes back from LDS).
         if (parser)
@@ -1392,7 +1384,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
             descriptors_ready<kOps>(S, len);
             tile_geometry_a<Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
-            if (report && mode_b_worthy(T.blocks()) && lane == 0u) post_report(report);
+            if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
             if (T.P > 0) {
 #pragma unroll
                 for (int i = 0; i < kPfA; ++i) {
@@ -1456,7 +1448,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         uint64_t S;
         uint32_t len;
         tile_descriptors(tile, grp0, n, offsets, lengths, S, len, fpt);
-        build_region_a<true>(tabs, lds);
+        build_region_a(tabs, lds);
         descriptors_ready<kOps>(S, len);
         U.P = 0;
         if (first) tile_geometry(T, U, tile, grp0, gl0, n, S, len, frames, lds, ws, fpt);
@@ -1500,10 +1492,8 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             asm volatile("" : "+v"(grp), "+v"(gl));
             uint32_t A[4] = {0u, 0u, 0u, 0u};
             uint32_t cs = 0u;
-            // general block: per row (scalar branches) the masked path (rows below H), the tail
-            // check (rows from Lt on: some piece ends there) or a lean row; rows past the pass's
-            // last row are skipped (a partial last block); refills reload the piece's last block
-            // for rows past it. kRefill: this pass's rows kPrefetch ahead (false: the last block).
+            // general block: rows below H take the masked path (scalar branch per row); refills
+            // of rows below H are clamped
             auto block = [&](int r0, auto refill_tag) {
                 constexpr bool kRefill = decltype(refill_tag)::value;
 #pragma unroll
@@ -1512,29 +1502,45 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
                     const int rel = U.rel0 + kRowDwords * r;
                     // consume the ring slot, then refill the SAME registers: no copy of an
                     // in-flight load, so the compiler keeps kPrefetch-1 loads outstanding
-                    if (r < U.H) masked_row_al(lds, keys, pf[i], rel, U.ndp, T.sa(), U.tmask, A, cs);
-                    else if (r < U.P && r >= U.Lt) tail_row_al(lds, keys, pf[i], rel, U.ndp, U.tmask, A, cs);
-                    else if (r < U.P) lean_row(lds, keys, pf[i], A, cs);
-                    if (kRefill) pf[i] = unit_row(U, r + kPrefetch);
+                    if (r < U.H) masked_row(lds, keys, pf[i], rel, load_pos(rel, U.lo), T.nd(), T.sa(), T.tail_mask(), A, cs);
+                    else lean_row(lds, keys, pf[i], A, cs);
+                    if (kRefill) {
+                        const int rn = rel + kRowDwords * kPrefetch;
+                        pf[i] = load_row(U.gfb, r + kPrefetch < U.H ? load_pos(rn, U.lo) : rn);
+                    }
+                }
+            };
+            // lean block: every row lean for every lane; the refills lie inside the frame, so they
+            // need no clamp: one pointer per block, immediate row offsets
+            auto lean_block = [&](int r0, auto refill_tag) {
+                constexpr bool kRefill = decltype(refill_tag)::value;
+                const uint32_t* pb = U.gfb + (U.rel0 + kRowDwords * (r0 + kPrefetch));
+#pragma unroll
+                for (int i = 0; i < kPrefetch; ++i) {
+                    lean_row(lds, keys, pf[i], A, cs);
+                    if (kRefill) pf[i] = *reinterpret_cast<const u32x4_a4*>(pb + kRowDwords * i);
+                    // keep consume/refill interleaved per row: unfenced, the scheduler sinks all
+                    // refills to the block end behind a vmcnt(0), draining the ring every block
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             };
             using Yes = std::true_type;
             using No = std::false_type;
+            const int Rc = U.P - kPrefetch;  // first row of the last block
             if (U.P > 0) {
-                // [first block] (pass 0: parse) [body: lean where it can] [last block, partial]
-                const int Pr = (U.P + kPrefetch - 1) / kPrefetch * kPrefetch;
-                const int Rc = Pr - kPrefetch;  // first row of the last block
-                // One block kind for every block of every pass (its per-row scalar branches pick the
-                // row's path): a join of two block kinds (lean blocks with immediate row offsets
-                // beside general ones) made hipcc copy the ring between register sets there, each
-                // copy waiting for its load -- a drained ring per pass
-                if (Pr > kPrefetch) {
-                    block(0, Yes());
+                // [first block] (pass 0: parse) [head blocks: general] [body: lean] [last block]
+                if (Rc > 0) {
+                    if (U.H > 0) block(0, Yes());
+                    else lean_block(0, Yes());
                     if (pass == 0) parse(true);
-                    for (int r0 = kPrefetch; r0 < Rc; r0 += kPrefetch) block(r0, Yes());
-                    block(Rc, No());
+                    int r0 = kPrefetch;
+                    for (; r0 < Rc && r0 < U.H; r0 += kPrefetch) block(r0, Yes());
+                    for (; r0 < Rc; r0 += kPrefetch) lean_block(r0, Yes());
+                    if (Rc < U.H) block(Rc, No());
+                    else lean_block(Rc, No());
                 } else {
-                    block(0, No());
+                    if (U.H > 0) block(0, No());
+                    else lean_block(0, No());
                     if (pass == 0) parse(false);
                 }
             } else {
@@ -1544,21 +1550,33 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             // Opaque frame descriptor: what the combine and the finish derive from it is
             // recomputed here rather than kept (and spilled) across the row loop.
             asm volatile("" : "+v"(T.S), "+v"(T.len));
+            // The pass's last row was lean (unless every row was masked): if it ends the frame,
+            // its last dword -- lane 3's 4th -- still holds the up to 3 bytes past the frame end.
+            // Their CRC contribution is that junk itself (the last dword enters the combine
+            // unshifted) and their sum is sad16 of it: combine_piece removes both.
+            uint32_t junk = 0u;
+            if (pass == 0) {
+                // mode B: a head piece ends the frame only when it is the whole frame
+                const bool ends = npass == 1 || pieces_of(T.nd()) == 1;
+                if (U.P > 0 && U.H < U.P && gl == 3u && T.nd() > 0 && ends) junk = pf[kPrefetch - 1].w & ~T.tail_mask();
+            } else if ((U.info & 0x40000000u) && gl == 3u) {
+                const uint32_t t = (U.info >> 28) & 3u;
+                junk = pf[kPrefetch - 1].w & ~(t == 0u ? 0xffffffffu : ((1u << (8u * t)) - 1u));
+            }
             const uint32_t info = U.info;
-            const int esh = U.esh;
             // the next pass's piece and its first rows, in flight during this pass's combine
             if (pass + 1 < npass) {
                 full_piece_unit(U, lds, ws, frames, T.F, pass + 1, grp, gl);
                 prefetch_unit(U, pf);
             }
-            uint32_t y;
-            combine_al(lds, gl, A, cs, esh, y);
+            uint32_t y, c;
+            combine_piece(lds, gl, A, cs, junk, y, c);
             if (npass == 1) {
                 Y = y;
-                csum = cs;
+                csum = c;
             } else if (gl == 0u && (pass == 0 || (info >> 31))) {
                 const uint32_t slot = pass == 0 ? grp : (info & 0xffffu);
-                *reinterpret_cast<uint2*>(lds + ws.slots + 8u * slot) = make_uint2(y, cs);
+                *reinterpret_cast<uint2*>(lds + ws.slots + 8u * slot) = make_uint2(y, c);
             }
         }
         FS_STAMP(3);
@@ -1569,13 +1587,12 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
                 const uint2 h = *reinterpret_cast<const uint2*>(lds + ws.slots + 8u * grp);
                 Y = h.x;
                 csum = h.y;
-                const Geo g = frame_geo(frames, T.S, T.len);
+                const int npc = pieces_of(T.nd());
                 // the frame's first full piece: the exclusive prefix of the groups' full pieces
-                const int e0 = (int)lds32(lds, ws.epre + 4u * grp) - (g.npc - 1);
-                for (int k = 1; k < g.npc; ++k) {
+                const int e0 = (int)lds32(lds, ws.epre + 4u * grp) - (npc - 1);
+                for (int k = 1; k < npc; ++k) {
                     const uint2 sl = *reinterpret_cast<const uint2*>(lds + ws.slots + 8u * (kFramesPerTile + e0 + k - 1));
-                    // between pieces that end on a block boundary Z768; into the last one Z_(768 - 4e)
-                    Y = (k + 1 < g.npc ? zplain(lds, Y, kLdsZ768) : z_last_piece(lds, Y, g.e)) ^ sl.x;
+                    Y = zplain(lds, Y, kLdsZ768) ^ sl.x;
                     csum += sl.y;
                 }
             }

@@ -212,87 +212,6 @@ def crc32_model_al(buf: bytes, S: int, length: int, base_phase: int = 0) -> int:
     return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
 
 
-def _combine_al(A, esh):
-    """combine_al: stream j of lane l shifted to the piece's last dword (q = 15 - esh)."""
-    q = 15 - esh
-    Y = 0
-    for lane in range(4):
-        K = (q - 4 * lane) & 15
-        a, C = K >> 2, K & 3
-        B = [A[lane][(C - c) & 3] for c in range(4)]
-        T = [B[0]] + [apply(op_table(4 * c), B[c]) for c in (1, 2, 3)]
-        V1 = V2 = 0
-        for c in range(4):
-            if c <= C:
-                V1 ^= T[c]
-            else:
-                V2 ^= T[c]
-        a2 = (a - 1) & 3
-        Y ^= (apply(op_table(16 * a), V1) if a else V1) ^ (apply(op_table(16 * a2), V2) if a2 else V2)
-    return Y
-
-
-def crc32_model_pieces(buf: bytes, S: int, length: int, base_phase: int = 0, mode_b: bool = True,
-                       pass0_rows: int = 0) -> int:
-    """digest_kernel_ab (the mixed-length kernel, round 5): block-aligned rows; the frame's B blocks
-    cut into a head piece of hb blocks (2 <= hb <= 13, hb = B for B <= 13) and npc - 1 full pieces of
-    12 blocks (mode_b), or one piece of B blocks (mode A). The head piece runs START-anchored in
-    pass 0 (pass0_rows >= hb rows: rows past the piece leave the streams untouched); each piece's
-    streams are combined to the piece's last dword (esh = e for the frame's last piece, 0 else) and
-    the pieces folded with Z768 between them and Z704 . Z_(64 - 4e) into the last one."""
-    E = S + length
-    if length < 4:
-        return crc32_model(buf, S, length)
-    sdw = S >> 2
-    nd = ((E + 3) >> 2) - sdw
-    sa = S & 3
-    te = (E & 3) or 4
-    head_mask = (0xFFFFFFFF << (8 * sa)) & 0xFFFFFFFF
-    tail_mask = 0xFFFFFFFF if te == 4 else (1 << (8 * te)) - 1
-    padded = b"\0" * 64 + bytes(buf) + b"\0" * 72
-    ph = (base_phase + sdw) & 15
-    e = (16 - ((ph + nd) & 15)) & 15
-    B = (ph + nd + e) // 16
-    npc = (B - 1 + 11) // 12 if (mode_b and B > 1) else 1
-    hb = B - 12 * (npc - 1)
-
-    def dword(rel):
-        return struct.unpack_from("<I", padded, 64 + 4 * (sdw + rel))[0]
-
-    def piece(b0, nb, rows, last):
-        ndp = nd if last else 16 * (b0 + nb) - ph
-        tm = tail_mask if last else 0xFFFFFFFF
-        A = [[0] * 4 for _ in range(4)]
-        for r in range(rows):
-            for lane in range(4):
-                rel = 16 * (b0 + min(r, nb - 1)) - ph + 4 * lane  # rows past the piece reload its last block
-                x0 = 16 * (b0 + r) - ph + 4 * lane
-                for j in range(4):
-                    x = x0 + j
-                    d = dword(rel + j) if x >= 0 else 0  # (a reloaded block is never streamed: x >= ndp)
-                    c = 0
-                    if x == 0:
-                        d &= head_mask
-                        c = head_mask
-                    if x == 1:
-                        c = ~head_mask & 0xFFFFFFFF
-                    if x == ndp - 1:
-                        d &= tm
-                    if x < ndp:
-                        A[lane][j] = apply(Z64, A[lane][j]) ^ d ^ c
-        return _combine_al(A, e if last else 0)
-
-    Y = piece(0, hb, max(pass0_rows, hb), npc == 1)
-    for k in range(1, npc):
-        y = piece(hb + 12 * (k - 1), 12, 12, k == npc - 1)
-        if k < npc - 1:
-            Y = apply(op_table(768), Y) ^ y
-        else:
-            Y = (apply(op_table(704), apply(op_table(64 - 4 * e), Y)) if e else apply(op_table(768), Y)) ^ y
-    t = (4 - (E & 3)) & 3
-    return apply(ZFIN[t], Y) ^ 0xFFFFFFFF
-
-
 Z8 = op_table(8)
 
 

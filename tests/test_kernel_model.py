@@ -102,21 +102,3 @@ def test_lane_per_frame_crc_vs_zlib():
             want = zlib.crc32(buf[S:S + length])
             for chains in (1, 2):
                 assert crc32_model_lane(buf, S, length, chains) == want, (S, length, chains)
-
-
-def test_block_aligned_pieces_vs_zlib():
-    """The mixed-length kernel (round 5): block-aligned head piece start-anchored in a longer pass 0,
-    12-block full pieces, the combine to each piece's last dword and the fold (Z768, then
-    Z704 . Z_(64 - 4e) into the last piece) reproduce zlib at every block phase, around the piece
-    boundaries (B = 12k + 1, 12k + 2) and at jumbo lengths."""
-    rnd = random.Random(13)
-    lengths = [4, 5, 63, 64, 65, 700, 767, 768, 769, 770, 800, 1500, 1536, 1537, 2300, 9000]
-    lengths += [rnd.randrange(4, 3000) for _ in range(6)]
-    for L in lengths:
-        for _ in range(3):
-            pre = rnd.randrange(0, 70)
-            buf = rnd.randbytes(pre + L + 8)
-            want = zlib.crc32(buf[pre : pre + L])
-            ph = rnd.randrange(16)
-            assert km.crc32_model_pieces(buf, pre, L, ph, mode_b=True, pass0_rows=rnd.randrange(0, 14)) == want, (L, pre, ph)
-            assert km.crc32_model_pieces(buf, pre, L, ph, mode_b=False, pass0_rows=0) == want, (L, pre, ph)
