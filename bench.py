@@ -163,8 +163,8 @@ def parse():
                    help="device pre-warm: when --warmup is below this, (min-warm - warmup) extra untimed "
                         "launches run first, over the streams, without the gather (reported as prewarm_launches)")
     p.add_argument("--kernel", type=int, default=None,
-                   help="fs_ctx_set_kernel variant: 0 automatic, 2 mixed-length, 4 one-pass, 8 small-frame (default: "
-                        "0; --config small: 8, the variant a caller with short-frame traffic selects)")
+                   help="fs_ctx_set_kernel variant: 0 automatic (default; short-frame traffic moves it to the "
+                        "small-frame kernel), 2 mixed-length, 4 one-pass, 8 small-frame preferred")
     p.add_argument("--workgroups", type=int, default=0,
                    help="fs_ctx_set_workgroups: workgroups per launch (0: one per CU; fewer give each wave several "
                         "tiles and let consecutive launches run side by side)")
@@ -346,7 +346,7 @@ def main():
     n = args.frames or 65536
     engine = GPU.engine(local)
     if args.kernel is None:
-        args.kernel = 8 if args.config == "small" else 0
+        args.kernel = 0
     engine.set_kernel(args.kernel)
     if args.workgroups:
         engine.set_workgroups(args.workgroups)
@@ -603,10 +603,11 @@ def main():
                                 "the line two neighbouring frames share is fetched twice (~8.4% on C2); "
                                 "traffic_calibrated divides that pattern factor out (the kernel's excess beyond it)"
                 if traffic is not None else None,
-                "kernel": {0: "automatic: digest_kernel_a (one-pass) for uniform batches, digest_kernel_ab for mixed",
+                "kernel": {0: "automatic: digest_kernel_a (one-pass) for uniform batches, digest_kernel_ab for mixed, "
+                              "digest_kernel_s once the launches it has seen ran had no frame over 128 B",
                            2: "digest_kernel_ab (mixed-length)", 4: "digest_kernel_a (one-pass)",
-                           8: "digest_kernel_s (small-frame, one lane per frame: fs_ctx_set_kernel 8, the caller's "
-                              "choice for short-frame traffic)"}.get(args.kernel),
+                           8: "digest_kernel_s preferred (fs_ctx_set_kernel 8: until a launch meets a frame over 128 B, "
+                              "then the automatic choice until short traffic resumes)"}.get(args.kernel),
                 "kernel_chosen": {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine_last_kernel),
                 "kernel_avg_us": round(k_avg_ms * 1e3, 3),
                 "kernel_timing": "HIP events around K back-to-back launches on the launch stream",
@@ -750,12 +751,13 @@ def sub_record_c3(args, dev):
 def sub_record_small(args, dev):
     """The reference's own benchmark shape beside the headline (stacks/benchmark_test.go:12-46: 47-B
     UDP 'hello' frames through RecvEth): 65,536 frames in 48-B slots, 4 resident batches, the
-    small-frame kernel (fs_ctx_set_kernel 8, the variant a caller with short-frame traffic selects),
-    the same steps and warmup as the headline. Frames/s is its natural unit."""
+    automatic kernel choice (variant 0: after the launches it has seen run with no frame over 128 B,
+    the small-frame kernel; kernel_chosen shows what the timed launches ran), the same steps and
+    warmup as the headline. Frames/s is its natural unit."""
     import torch
 
     engine = GPU.engine(0)
-    engine.set_kernel(8)
+    engine.set_kernel(0)  # the automatic choice: it moves to the small-frame kernel on this traffic
     t_start = time.perf_counter()
     n = 65536
     batches = []
@@ -846,9 +848,11 @@ def sub_record_small_host(args):
     n, nbytes = len(ln), int(ln.astype(np.int64).sum())
     pin = eng.host_empty(buf.shape, np.uint8)
     pin[:] = buf
-    poff = eng.host_empty(off.shape, np.uint64)
+    # the offsets and then the lengths in one pinned block, as the Go binding stages them (one H2D copy)
+    desc = eng.host_empty((12 * n,), np.uint8)
+    poff = desc[: 8 * n].view(np.uint64)
+    plen = desc[8 * n:].view(np.uint32)
     poff[:] = off
-    plen = eng.host_empty(ln.shape, np.uint32)
     plen[:] = ln
     from seqs_amd.framesum import DIGEST_DTYPE
     out = np.zeros(n, dtype=DIGEST_DTYPE)

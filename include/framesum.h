@@ -150,9 +150,10 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
 /* Same computation from/to HOST memory (the NIC / loopback buffer handed to
  * RecvEth): stages H2D, runs the kernel and copies D2H on the context's
  * stream, returning when the results are in `out`/`status`. Pinned memory
- * (fs_host_alloc) gives full PCIe rate; pageable memory works. With the automatic
- * kernel choice (fs_ctx_set_kernel 0) a batch whose frames are all <= 128 bytes runs
- * the small-frame kernel (variant 8): the lengths are on the host here. */
+ * (fs_host_alloc) gives full PCIe rate; pageable memory works (offsets, lengths, out and status
+ * that are pinned are copied straight from / to, the others through the context's pinned mirror).
+ * With fs_ctx_set_kernel 0 or 8 a batch whose frames are all <= 128 bytes runs the small-frame
+ * kernel: the lengths are on the host here. */
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status);
 
@@ -222,22 +223,32 @@ uint64_t fs_shard_slab_bytes(uint64_t n, uint32_t nshards);
 fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards, uint64_t n, fs_digest* out,
                           uint8_t* status, void* stream);
 
-/* Kernel variant of a context's launches. The engine has two: a one-pass kernel
- * for batches of similar frame lengths (each frame read as the 64-byte blocks that
- * hold it), and one that splits long frames into 768-byte pieces when a tile of 16
- * frames mixes very different lengths. By default (variant 0) every launch reports
- * whether its batch had such tiles and the next launch picks accordingly. 2 forces
- * the mixed-length kernel, 4 the one-pass kernel, 8 the small-frame kernel (one lane per
- * frame, small workgroups: for traffic of short frames such as the reference's 47-byte
- * benchmark frames; fs_digest_batch* and fs_digest_batch_fcs run it, a TX fill runs the
- * automatic choice; frames longer than ~130 bytes stay correct but are slow there); any
- * other value is FS_E_INVALID. Results are identical in every case; only the speed differs. */
+/* Kernel variant of a context's launches. The engine has three kernels: a one-pass kernel for
+ * batches of similar frame lengths (each frame read as the 64-byte blocks that hold it), a
+ * mixed-length kernel that splits long frames into 768-byte pieces when a tile of 16 frames mixes
+ * very different lengths, and a small-frame kernel (one lane per frame, small workgroups) for
+ * traffic of short frames such as the reference's 47-byte benchmark frames. The kernels report,
+ * per launch, whether its batch had mixed-length tiles and whether it had a frame longer than 128
+ * bytes; the host reads those reports a few launches late.
+ *   0 (default): automatic. Mixed-length tiles select the mixed-length kernel, similar lengths the
+ *     one-pass kernel; after 16 launches seen to run with no frame over 128 bytes, the small-frame
+ *     kernel, until a launch reports a longer frame.
+ *   2 / 4: always the mixed-length / the one-pass kernel.
+ *   8: the small-frame kernel preferred: it runs until a launch reports a frame over 128 bytes,
+ *     then the automatic choice between the other two until 2 launches have run short again.
+ * The host-staged calls see every length: with 0 or 8 a batch whose frames are all <= 128 bytes
+ * runs the small-frame kernel, any other batch the automatic choice. A TX fill never runs the
+ * small-frame kernel. Because reports arrive late, a launch of the small-frame kernel can still meet
+ * long frames: they stay correct there but one lane streams each of them (hundreds of us for a
+ * batch of jumbo frames). Any other variant is FS_E_INVALID. Results are identical in every case;
+ * only the speed differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
-/* The variant (2, 4 or 8, as above) the context's latest launch ran; 0 before its first
- * launch, FS_E_INVALID for a null context. With variant 0 a context's first 16
- * launches run the mixed-length kernel (2), which keeps itself chosen while it
- * meets mixed tiles; uniform traffic then moves to the one-pass kernel (4). */
+/* The kernel (2 mixed-length, 4 one-pass, 8 small-frame) the context's latest launch ran; 0 before
+ * its first launch, FS_E_INVALID for a null context. With variant 0 a context's first 16 launches
+ * run the mixed-length kernel (2), which keeps itself chosen while it meets mixed tiles; uniform
+ * traffic then moves to the one-pass kernel (4), and traffic of frames <= 128 bytes to the
+ * small-frame kernel (8). */
 int fs_ctx_last_kernel(const fs_ctx* ctx);
 
 /* Workgroups per launch of a context's kernels: 0 (the default) launches one 16-wave

@@ -71,6 +71,7 @@ struct fs_ctx {
     // pinned host mirrors of the descriptors and results, so every per-chunk copy is
     // asynchronous even when the caller's arrays are pageable (Go slices, numpy)
     uint8_t* h_pin = nullptr;
+    uint8_t* d_pin = nullptr;  // h_pin as the device addresses it (mapped): kernels write results there
     uint64_t cap_pin_n = 0;
     std::string err;
 };
@@ -141,9 +142,15 @@ fs_status ensure_pinned(fs_ctx* ctx, uint32_t n) {
     if (n <= ctx->cap_pin_n) return FS_SUCCESS;
     if (ctx->h_pin) FS_HIP(ctx, hipHostFree(ctx->h_pin));
     ctx->h_pin = nullptr;
+    ctx->d_pin = nullptr;
     ctx->cap_pin_n = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pin), (size_t)n * 21 + 64, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pin), (size_t)n * 21 + 64, hipHostMallocMapped) != hipSuccess)
         return set_err(ctx, FS_E_NOMEM, "hipHostMalloc descriptor mirror");
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_pin), ctx->h_pin, 0) != hipSuccess) {
+        (void)hipHostFree(ctx->h_pin);
+        ctx->h_pin = nullptr;
+        return set_err(ctx, FS_E_HIP, "hipHostGetDevicePointer of the descriptor mirror");
+    }
     ctx->cap_pin_n = n;
     return FS_SUCCESS;
 }
@@ -199,11 +206,16 @@ hipError_t launch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, c
                                    force >= 0 ? force : ctx->force_kernel, op, wframes, tx);
 }
 
-// The host-staged digest sees the batch's lengths on the host: with the automatic choice, a batch
-// whose frames are all this short runs the small-frame kernel (variant 8, one lane per frame; its
-// header slot holds frames up to ~130 B). A device-resident batch's lengths are in device memory:
-// there the caller selects it (fs_ctx_set_kernel).
-constexpr uint32_t kSmallAutoMaxLen = 128;
+// The host-staged digest sees the batch's lengths on the host: with the automatic choice (0) or the
+// short-frame preference (8), a batch whose frames are all this short runs the small-frame kernel
+// (one lane per frame; its header slot holds frames up to ~130 B), and any other batch the
+// automatic choice between the 4-lane kernels. (A device-resident batch's lengths are in device
+// memory: there launch_digest chooses from the kernels' reports.)
+constexpr uint32_t kSmallAutoMaxLen = framesum::kSmallMaxLen;
+int host_force(const fs_ctx* ctx, uint32_t max_len) {
+    if (ctx->force_kernel != 0 && ctx->force_kernel != 8) return ctx->force_kernel;
+    return max_len <= kSmallAutoMaxLen ? framesum::kForceSmallExact : 0;
+}
 
 }  // namespace
 
@@ -253,6 +265,9 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
             ctx->h_report[framesum::kReportChosen] = 0u;
             ctx->h_report[framesum::kReportSeen] = 0u;
             ctx->h_report[framesum::kReportSeenSeq] = 0u;
+            for (int w : {framesum::kReportLong, framesum::kReportRan, framesum::kReportLongSeen,
+                          framesum::kReportRanSeen, framesum::kReportShort})
+                ctx->h_report[w] = 0u;
             e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_report), hp, 0);
         }
     }
@@ -368,44 +383,53 @@ FS_HOST_CLONES static framesum::plan::ScanCore scan_descriptors(const uint64_t* 
 // the frames and one of the descriptors on the two copy streams at once, one launch, the results'
 // D2H, and a polled wait. Descriptors and results go straight from / to the caller's arrays when
 // those are pinned (fs_host_alloc), through the context's pinned mirror otherwise.
+// The device address of pinned host memory the kernel can write its results to directly, or null.
+static void* mapped(void* p) {
+    if (!p || !is_pinned(p)) return nullptr;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return d;
+}
+
 static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                              const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status,
-                             const framesum::plan::Scan& sc, int force, bool pin_desc) {
+                             const framesum::plan::Scan& sc, int force) {
     uint64_t cpy_lo, cpy_hi;
     framesum::plan::copy_span(sc.lo, sc.hi, frames_bytes, cpy_lo, cpy_hi);
     HostSlot& sl = ctx->slot[0];
     fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, n);
     if (st != FS_SUCCESS) return st;
-    const bool pin_out = is_pinned(out) && (!status || is_pinned(status));
-    fs_digest* h_out = pin_out ? out : reinterpret_cast<fs_digest*>(ctx->h_pin + (size_t)n * 12);
-    uint8_t* h_st = pin_out ? status : ctx->h_pin + (size_t)n * 20;  // (right after h_out in the mirror)
+    // The kernel writes the digests and verdicts straight to host memory (mapped pinned memory: no
+    // D2H copy, no gap before it): into the caller's arrays when they are pinned, else into the
+    // context's pinned mirror, copied out after the wait.
+    void* d_out = mapped(out);
+    void* d_st = status ? mapped(status) : nullptr;
+    const bool direct = d_out && (!status || d_st);
+    if (!direct) {
+        d_out = ctx->d_pin + (size_t)n * 12;
+        d_st = status ? ctx->d_pin + (size_t)n * 20 : nullptr;
+    }
     const hipStream_t ks = ctx->compute_stream;
-    // the frames behind the descriptors (issued by the caller before the scan), then the kernel and
-    // the results, all in the compute stream's order: no cross-stream event between them
+    // the frames behind the descriptors (issued by the caller before the scan), then the kernel, in
+    // the compute stream's order: no cross-stream event between them
     FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, ks));
     if (ctx->fault_chunk == 0) return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: injected failure (test hook)");
     const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
     const uint64_t* d_off = reinterpret_cast<const uint64_t*>(ctx->d_desc);
     const uint32_t* d_len = reinterpret_cast<const uint32_t*>(ctx->d_desc + (size_t)n * 8);
-    // digests and verdicts back to back in the slot (d_status = d_out + 8 n): one D2H of 9 n bytes
-    uint8_t* d_res = reinterpret_cast<uint8_t*>(sl.d_out);
-    FS_HIP(ctx, launch(ctx, base, d_off, d_len, n, mtu, sl.d_out, status ? d_res + (size_t)n * 8 : nullptr, ks,
-                       framesum::FsOp::kDigest, nullptr, 0, force));
+    FS_HIP(ctx, launch(ctx, base, d_off, d_len, n, mtu, reinterpret_cast<fs_digest*>(d_out),
+                       reinterpret_cast<uint8_t*>(d_st), ks, framesum::FsOp::kDigest, nullptr, 0, force));
     FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
     sl.used = true;
-    if (pin_out) {
-        FS_HIP(ctx, hipMemcpyAsync(h_out, d_res, (size_t)n * sizeof(fs_digest), hipMemcpyDeviceToHost, ks));
-        if (status) FS_HIP(ctx, hipMemcpyAsync(h_st, d_res + (size_t)n * 8, n, hipMemcpyDeviceToHost, ks));
-    } else {
-        FS_HIP(ctx, hipMemcpyAsync(h_out, d_res, (size_t)n * (status ? 9 : 8), hipMemcpyDeviceToHost, ks));
-    }
     FS_HIP(ctx, hipEventRecord(ctx->host_done, ks));
     FS_HIP(ctx, host_wait(ctx->host_done));
-    if (!pin_out) {
-        std::memcpy(out, h_out, (size_t)n * sizeof(fs_digest));
-        if (status) std::memcpy(status, h_st, n);
+    if (!direct) {
+        std::memcpy(out, ctx->h_pin + (size_t)n * 12, (size_t)n * sizeof(fs_digest));
+        if (status) std::memcpy(status, ctx->h_pin + (size_t)n * 20, n);
     }
-    (void)pin_desc;
     ctx->host_dirty = false;
     return FS_SUCCESS;
 }
@@ -454,16 +478,16 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
             ctx->host_dirty = false;
             return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
         }
-        const int force = ctx->force_kernel == 0 && sc.max_len <= kSmallAutoMaxLen ? 8 : ctx->force_kernel;
+        const int force = host_force(ctx, sc.max_len);
         if (sc.hi - sc.lo <= kChunkBytes)
-            return host_single(ctx, frames, frames_bytes, offsets, lengths, n, mtu, out, status, sc, force, pin_desc);
+            return host_single(ctx, frames, frames_bytes, offsets, lengths, n, mtu, out, status, sc, force);
         FS_HIP(ctx, hipStreamSynchronize(ks));  // (the chunked path below stages the descriptors itself)
     }
     const framesum::plan::Scan sc =
         framesum::plan::scan_from(scan_descriptors(offsets, lengths, n), offsets, lengths, n, frames_bytes);
     if (sc.bad < n)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
-    const int force = ctx->force_kernel == 0 && sc.max_len <= kSmallAutoMaxLen ? 8 : ctx->force_kernel;
+    const int force = host_force(ctx, sc.max_len);
     ctx->host_dirty = true;  // until this call has waited for all of its work
     pst = ensure_pinned(ctx, n);
     if (pst != FS_SUCCESS) return pst;
@@ -739,6 +763,14 @@ int fs_ctx_last_kernel(const fs_ctx* ctx) {
 fs_status fs_test_set_fault(fs_ctx* ctx, long chunk) {
     if (!ctx) return FS_E_INVALID;
     ctx->fault_chunk = chunk;
+    return FS_SUCCESS;
+}
+// ... and the context's kernel choice set to any launch_digest force value, e.g. kForceSmallExact (16):
+// the small-frame kernel for every launch, whatever the reports say (the parity suite's
+// "small_exact" column runs every case through that kernel's own long-frame path).
+fs_status fs_test_set_kernel_exact(fs_ctx* ctx, int force) {
+    if (!ctx) return FS_E_INVALID;
+    ctx->force_kernel = force;
     return FS_SUCCESS;
 }
 #endif

@@ -58,6 +58,23 @@ enum class FsOp { kDigest, kFill, kFcs };
 // change, and the context's launch sequence at that moment (the sticky window's clock).
 constexpr int kReportLatest = 0, kReportInitial = 1, kReportChosen = 2, kReportSeen = 3, kReportSeenSeq = 4;
 constexpr uint32_t kInitialMixedLaunches = 16;
+// The short-frame choice (the small-frame kernel, variant 8, for traffic of frames <= kSmallMaxLen
+// bytes): kReportLong and kReportRan are written by the device -- the latest launch
+// id that met a frame longer than kSmallMaxLen, and the latest launch id that ran a 4-lane kernel
+// (its first workgroup, after that workgroup has posted its own long flag); kReportLongSeen,
+// kReportRanSeen and kReportShort only by the host: the two words as it last saw them and the
+// number of launches seen to run since the latest long report (launch_digest).
+constexpr int kReportLong = 5, kReportRan = 6, kReportLongSeen = 7, kReportRanSeen = 8, kReportShort = 9;
+constexpr uint32_t kSmallMaxLen = 128;
+// the kernels' `report` argument: the report block's device address in bits 0..46 (host-mapped
+// memory sits below 2^47), a watch flag in bit 47, the launch id in bits 48..63
+constexpr uint64_t kReportAddrMask = (1ull << 47) - 1u;
+// launches seen to run without a long frame before variant 0 moves to the small-frame kernel, and
+// before a variant-8 context that met long frames goes back to it
+constexpr uint32_t kShortLaunchesAuto = 16, kShortLaunchesSmall = 2;
+// launch_digest's force value for the host-staged path, which knows every length: the small-frame
+// kernel unconditionally
+constexpr int kForceSmallExact = 16;
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
                          int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, uint32_t* next_id,

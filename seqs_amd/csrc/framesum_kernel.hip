@@ -102,7 +102,11 @@ static_assert(kTablesLdsBytes == kLdsTables, "FsTables is the LDS image of the t
 
 // The workgroup's LDS image (static allocation of the digest kernels). Namespace scope, so the
 // out-of-line parse routine addresses it as LDS (ds_read), not through a flat pointer.
-__shared__ __attribute__((aligned(16))) char g_lds[kLdsBytes];
+// Per-wave report flags of a workgroup's first tiles (bit 0: a frame longer than kSmallMaxLen; bit 1:
+// a tile worth mode B), read by wave 0 after the preamble barrier: one post per workgroup.
+constexpr uint32_t kLdsFlags = kLdsBytes;
+constexpr uint32_t kFlagLong = 1u, kFlagMixed = 2u;
+__shared__ __attribute__((aligned(16))) char g_lds[kLdsBytes + 4 * kWavesPerBlock];
 
 #ifdef FS_STAMPS
 // Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
@@ -1117,17 +1121,42 @@ struct LayA1 : LayoutA {
     }
 };
 
-// `report` = the host-mapped report word's address in bits 0..47, the launch id in bits 48..63
+// `report` = the host-mapped report block's address in bits 0..46, the watch flag in bit 47, the launch
+// id in bits 48..63
 // (one kernel argument, loaded where it is used: nothing of it stays live through the tile loop).
+template <int kWord = kReportLatest>
 __device__ __forceinline__ void post_report(uint64_t report) {
     asm volatile("" : "+s"(report));  // split here, not hoisted into a register held by the whole kernel
     // a GLOBAL store (address space 1), not a flat one: hipcc's wait counting treats any pending
-    // flat op as able to complete out of order, so every vmcnt wait after it became vmcnt(0) --
-    // the first block of rows waited for the whole ring
+    // flat op as able to complete out of order with the vector memory operations, so every vmcnt
+    // wait after it became vmcnt(0) -- the first block of rows waited for the whole ring
     typedef __attribute__((address_space(1))) uint32_t gu32;
-    *reinterpret_cast<gu32*>(report & 0xFFFFFFFFFFFFull) = (uint32_t)(report >> 48);
+    *reinterpret_cast<gu32*>((report & kReportAddrMask) + 4u * kWord) = (uint32_t)(report >> 48);
+}
+// Bit 47 of `report`: the host is counting short launches (or a long report is news to it), so every
+// workgroup reports its long frames; otherwise only the first workgroup does, beside its "ran" post
+// (uniform long traffic then costs one post per launch, not one per workgroup).
+__device__ __forceinline__ bool report_watch(uint64_t report) { return ((report >> 47) & 1u) != 0u; }
+
+// A wave's report flags for its tile (frames of `len`, group-uniform; 0 for an empty group).
+__device__ __forceinline__ uint32_t tile_long(uint32_t len) {
+    return group_max((int)min(len, 0x7fffffffu)) > (int)kSmallMaxLen ? kFlagLong : 0u;
 }
 
+// After the preamble barrier: wave 0 posts its workgroup's first-tile flags (one store per flag that
+// is set; the first workgroup then posts that the launch ran, after its own long flag).
+__device__ __forceinline__ void post_workgroup(const char* lds, uint64_t report, uint32_t wave, uint32_t lane) {
+    if (!report || wave != 0u || lane != 0u) return;
+    uint32_t f = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kWavesPerBlock; j += 4) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(lds + kLdsFlags + 4u * j);
+        f |= v.x | v.y | v.z | v.w;
+    }
+    if ((f & kFlagLong) && (blockIdx.x == 0u || report_watch(report))) post_report<kReportLong>(report);
+    if (f & kFlagMixed) post_report<kReportLatest>(report);
+    if (blockIdx.x == 0u) post_report<kReportRan>(report);
+}
 // The wave's first tile (later tiles: + all waves): wave-major, so a workgroup's waves read tiles
 // spread over the batch and neighbouring workgroups (on different XCDs) neighbouring tiles.
 __device__ __forceinline__ uint32_t first_tile(uint32_t wave) { return wave * gridDim.x + blockIdx.x; }
@@ -1223,7 +1252,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         for (int i = 0; i < kPfA; ++i) pf[i] = load_row(T.gfb, lpos(T.rel0 + kRowDwords * i, T.lo));
     }
     if (first) tile_geometry_a_tail<Lay::kCapBlocks>(T);
-    if (first && report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+    // this wave's first-tile report flags, posted once per workgroup after the barrier
+    uint32_t wflags = 0u;
+    if (first && report) wflags = tile_long(T.len) | (mode_b_worthy(T.nd()) ? kFlagMixed : 0u);
+    if (lane == 0u) *reinterpret_cast<uint32_t*>(lds + kLdsFlags + 4u * wave) = wflags;
     if (first) tile_header(T);
     FS_STAMP(13);
     FS_STAMP(9);
@@ -1232,6 +1264,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     else __builtin_amdgcn_s_waitcnt(0x0070);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    post_workgroup(lds, report, __builtin_amdgcn_readfirstlane(wave), lane);
     // two-level age priority: the SIMD's younger half (waves 8..15) outranks the older (round 2:
     // -0.35..-0.55 us per launch)
     if ((__builtin_amdgcn_readfirstlane(wave) >> 3) != 0u) __builtin_amdgcn_s_setprio(1);
@@ -1385,6 +1418,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             descriptors_ready<kOps>(S, len);
             tile_geometry_a<Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
             if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
+            if (report && report_watch(report) && tile_long(T.len) && lane == 0u) post_report<kReportLong>(report);
             if (T.P > 0) {
 #pragma unroll
                 for (int i = 0; i < kPfA; ++i) {
@@ -1458,10 +1492,15 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     // is all the parse's vmcnt(kPrefetch) needs)
     if (first) prefetch_unit(U, pf);
     if (first) x4 = header_dma<false>(T, frames, lds, hw, gl0, lane);
+    // this wave's first-tile report flags, posted once per workgroup after the barrier
+    uint32_t wflags = 0u;
+    if (first && report) wflags = tile_long(T.len) | (T.npass > 1 ? kFlagMixed : 0u);
+    if (lane == 0u) *reinterpret_cast<uint32_t*>(lds + kLdsFlags + 4u * wave) = wflags;
     FS_STAMP(9);
     tables_landed<kPrefetch>(first, U.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    post_workgroup(lds, report, wave, lane);
     if ((wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // two-level age priority: the SIMD's younger half first
     FS_STAMP(1);
 
@@ -1475,7 +1514,6 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
         const bool fvalid = grp < fpt && tile * fpt + grp < n;
         const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
         const int npass = T.npass;
-        if (npass > 1 && lane == 0u && report) post_report(report);  // this launch met a mixed tile
 
         // ---- header parse: after the first block of rows, while the ring's loads are in flight.
         // The header DMA was issued before the tile's rows; vmcnt(kPrefetch) retires it once the
@@ -1611,6 +1649,11 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             tile_geometry(T, U, tile, grp, gl, n, S, len, frames, lds, ws, fpt);
             header_dma<false>(T, frames, lds, hw, gl, lane);
             prefetch_unit(U, pf);
+            // a later tile of this wave (the first tiles' flags went out with the workgroup's post)
+            if (report) {
+                if (T.npass > 1 && lane == 0u) post_report(report);  // this launch met a mixed tile
+                if (report_watch(report) && tile_long(T.len) && lane == 0u) post_report<kReportLong>(report);
+            }
         }
     }
 }
@@ -1661,7 +1704,7 @@ template <uint32_t kOps>
 __global__ void __launch_bounds__(kWave * kSmallWaves)
 digest_kernel_s(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
                 const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
-                uint2* __restrict__ out, uint8_t* __restrict__ status) {
+                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report) {
     static_assert(kOps != kOpsTx, "the small-frame kernel has no TX fill");
     char* lds = s_lds;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1697,9 +1740,16 @@ digest_kernel_s(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     }
     __syncthreads();
 
+    bool long_posted = false;
     for (; tile < ntiles; tile += nwaves) {
         const uint32_t fi = tile * 64u + lane;
         const bool valid = fi < n;
+        // a frame too long for this kernel's slot: report it (once per wave), so the launches that
+        // follow run the 4-lane kernels (launch_digest); this one stays correct, only slower
+        if (report && !long_posted && __ballot(valid && len > kSmallMaxLen) != 0u) {
+            if (lane == 0u) post_report<kReportLong>(report);
+            long_posted = true;
+        }
         if (kOps == kOpsFcs) len = len >= 4u ? len - 4u : 0u;
         // 16-B chunks at ABSOLUTE 16-B boundaries (frames is only 4-byte aligned): a chunk that
         // holds a frame byte never leaves that byte's page
@@ -1811,8 +1861,8 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     uint32_t id = seq & 0xFFFFu;
     if (id == 0u) id = 0x8000u;  // (0 means "never reported"; any non-zero tag will do)
     const uint64_t rdev = reinterpret_cast<uint64_t>(report_dev);
-    const bool can_report = report_host && rdev != 0u && (rdev >> 48) == 0u;
-    const uint64_t report = can_report ? rdev | ((uint64_t)id << 48) : 0u;
+    const bool can_report = report_host && rdev != 0u && (rdev & ~kReportAddrMask) == 0u;
+    uint64_t report = can_report ? rdev | ((uint64_t)id << 48) : 0u;
     bool mixed = false;
     if (can_report) {
         const uint32_t latest = report_host[kReportLatest];
@@ -1831,10 +1881,37 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
             mixed = true;
         }
     }
-    // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel, 8 the small-frame kernel
-    // (RX digest and FCS verify; a TX fill keeps the automatic choice above)
+    // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
     if (force == 2 || force == 4) mixed = force == 2;
-    const bool small = force == 8 && op != FsOp::kFill;
+    // The small-frame kernel (RX digest and FCS verify; a TX fill keeps the 4-lane choice above).
+    // The kernels report every launch that met a frame longer than kSmallMaxLen (kReportLong), and
+    // the 4-lane kernels every launch that ran (kReportRan, posted after its first workgroup's own
+    // long flag); the host counts the launches it sees run since the latest long report. Variant 0
+    // moves to the small-frame kernel after kShortLaunchesAuto of them; variant 8 runs it until a
+    // long report arrives, then the 4-lane choice until kShortLaunchesSmall launches ran short
+    // again. The reports come launches late, so a long frame can still meet the small-frame kernel:
+    // it stays correct there, only slower (one lane streams it). kForceSmallExact: the host-staged
+    // path, which has seen every length.
+    bool small = false;
+    if (can_report) {
+        const uint32_t lng = report_host[kReportLong], ran = report_host[kReportRan];
+        if (lng != report_host[kReportLongSeen]) {
+            report_host[kReportLongSeen] = lng;
+            report_host[kReportShort] = 0u;
+        } else if (ran != report_host[kReportRanSeen] && ran != lng && report_host[kReportShort] < (1u << 30)) {
+            report_host[kReportShort] = report_host[kReportShort] + 1u;
+        }
+        report_host[kReportRanSeen] = ran;
+        const uint32_t streak = report_host[kReportShort];
+        if (force == 0) small = streak >= kShortLaunchesAuto;
+        if (force == 8) small = lng == 0u || streak >= kShortLaunchesSmall;
+        // every workgroup reports its long frames while the host counts short launches
+        if ((force == 0 || force == 8) && streak > 0u) report |= 1ull << 47;
+    } else if (force == 8) {
+        small = true;  // no report block: the caller's choice as it stands
+    }
+    if (force == kForceSmallExact) small = true;
+    if (op == FsOp::kFill) small = false;
     if (small) mixed = false;
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {
@@ -1860,10 +1937,10 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         if (sb > 2u * max_blocks) sb = 2u * max_blocks;
         if (op == FsOp::kFcs)
             hipLaunchKernelGGL((digest_kernel_s<kOpsFcs>), dim3(sb), dim3(kWave * kSmallWaves), 0, stream, frames,
-                               offsets, lengths, n, mtu, tables, reinterpret_cast<uint2*>(out), status);
+                               offsets, lengths, n, mtu, tables, reinterpret_cast<uint2*>(out), status, report);
         else
             hipLaunchKernelGGL((digest_kernel_s<kOpsDigest>), dim3(sb), dim3(kWave * kSmallWaves), 0, stream, frames,
-                               offsets, lengths, n, mtu, tables, reinterpret_cast<uint2*>(out), status);
+                               offsets, lengths, n, mtu, tables, reinterpret_cast<uint2*>(out), status, report);
         return hipGetLastError();
     }
     switch (op) {

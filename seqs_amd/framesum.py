@@ -168,6 +168,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.fs_test_group_set_fault.argtypes = [vp, ctypes.c_long]
         lib.fs_test_group_set_fault_gather.restype = i32
         lib.fs_test_group_set_fault_gather.argtypes = [vp, ctypes.c_long]
+        lib.fs_test_set_kernel_exact.restype = i32
+        lib.fs_test_set_kernel_exact.argtypes = [vp, ctypes.c_int]
     _libs[p] = lib
     if path is None:
         _lib = lib
@@ -224,11 +226,13 @@ class Engine:
 
     def set_kernel(self, variant: int) -> None:
         """0 (KERNEL_AUTO): automatic (the mixed-length kernel after a batch that had mixed-length
-        tiles, the one-pass kernel otherwise); 2 (KERNEL_MIXED): the kernel that splits long frames
+        tiles, the one-pass kernel otherwise, the small-frame kernel for short-frame traffic); 2 (KERNEL_MIXED): the kernel that splits long frames
         of mixed-length tiles into pieces; 4 (KERNEL_ONE_PASS): the one-pass kernel (block-aligned
-        rows); 8 (KERNEL_SMALL): one lane per frame, for short-frame traffic (RX digest and FCS
-        verify; a TX fill then runs the automatic choice; long frames stay correct but slow). Any
-        other value raises."""
+        rows); 8 (KERNEL_SMALL): the small-frame kernel (one lane per frame) preferred: it runs until a
+        launch reports a frame over 128 B, then the automatic choice until short traffic resumes.
+        The automatic choice itself moves to the small-frame kernel after 16 launches seen to run
+        with no frame over 128 B (include/framesum.h). A TX fill never runs the small-frame kernel.
+        Any other value raises."""
         self._check(self.lib.fs_ctx_set_kernel(self._ctx, int(variant)), "fs_ctx_set_kernel")
 
     def set_workgroups(self, workgroups: int) -> None:

@@ -8,6 +8,8 @@ import random
 import numpy as np
 import pytest
 
+import engines  # noqa: E402
+
 import framegen
 from oracle import coracle
 
@@ -57,14 +59,11 @@ def _batch(phase: int, room: int):
     return _CACHE[key]
 
 
-@pytest.fixture(scope="module", params=[4, 2, 0, 8], ids=["one_pass", "mixed", "auto", "small"])
+@pytest.fixture(scope="module", params=engines.VARIANTS, ids=engines.IDS)
 def engine(request):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from seqs_amd import Engine
-
-    e = Engine(0)
-    e.set_kernel(request.param)
+    e = engines.engine_for(request.param)
     if request.param == 0:
         # a context's first 16 launches run the mixed-length kernel whatever the
         # batch, so without this the 'auto' column would re-test it. Uniform batches past that

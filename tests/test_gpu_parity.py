@@ -11,6 +11,8 @@ import zlib
 import numpy as np
 import pytest
 
+import engines  # noqa: E402
+
 torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
@@ -21,14 +23,12 @@ from seqs_amd import Engine, pack_frames, split_digests, synth  # noqa: E402
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(scope="module", params=[Engine.KERNEL_ONE_PASS, Engine.KERNEL_MIXED, Engine.KERNEL_AUTO,
-                                        Engine.KERNEL_SMALL], ids=["one_pass", "mixed", "auto", "small"])
+@pytest.fixture(scope="module", params=engines.VARIANTS, ids=engines.IDS)
 def engine(request):
     # every case through every kernel variant (and the automatic choice)
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    e = Engine(0)
-    e.set_kernel(request.param)
+    e = engines.engine_for(request.param)
     yield e
     e.close()
 
@@ -536,3 +536,98 @@ def test_host_fill_after_failed_digest():
         assert np.array_equal(got, exp) and np.array_equal(dig, edig) and np.array_equal(st, est)
     finally:
         e.close()
+
+
+def _dev_batch(buf, off, ln):
+    dev = torch.device("cuda:0")
+    return (torch.from_numpy(np.ascontiguousarray(buf)).to(dev),
+            torch.from_numpy(np.ascontiguousarray(off).astype(np.int64)).to(dev),
+            torch.from_numpy(np.ascontiguousarray(ln).astype(np.int32)).to(dev))
+
+
+def _exact(out, st, buf, off, ln, label, mtu=0):
+    crc, ipc, l4c = split_digests(out.cpu().numpy())
+    st = st.cpu().numpy()
+    dig, est = coracle.digest_batch(buf, off, ln, mtu=mtu, nthreads=8)
+    bad = np.nonzero((crc != dig["crc32"]) | (ipc != dig["ip_csum"]) | (l4c != dig["l4_csum"]) | (st != est))[0]
+    assert bad.size == 0, f"{label}: {bad.size} mismatches, first at {int(bad[0])}"
+
+
+def test_auto_choice_short_frames_device():
+    """variant 0 on device-resident batches moves to the small-frame kernel
+    after kShortLaunchesAuto launches it has seen run with no frame over 128 B, leaves it on the
+    first long report, and comes back when short traffic resumes. Short (47-B) and jumbo (9000-B)
+    batches alternate; every launch's results are bit-exact against the oracle whichever kernel ran."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    e = Engine(0)
+    try:
+        sb, so, sl = synth.hello_batch(8192, seed=21)
+        jb, jo, jl = synth.uniform_batch(1024, 9000, seed=22)
+        ts, tj = _dev_batch(sb, so, sl), _dev_batch(jb, jo, jl)
+        seen = []
+
+        def run(t, host, label, k=1):
+            for _ in range(k):
+                out, st = e.digest_device(*t)
+                torch.cuda.synchronize()  # the launch's reports are in before the next launch chooses
+                seen.append(e.last_kernel())
+                _exact(out, st, *host, label)
+
+        run(ts, (sb, so, sl), "short warm-up", 40)
+        assert seen[-1] == Engine.KERNEL_SMALL, seen
+        assert Engine.KERNEL_SMALL not in seen[:16], seen  # not before the initial window and the count
+        run(tj, (jb, jo, jl), "jumbo after short", 4)
+        assert seen[-1] in (Engine.KERNEL_MIXED, Engine.KERNEL_ONE_PASS), seen[-6:]
+        run(ts, (sb, so, sl), "short again", 24)
+        assert seen[-1] == Engine.KERNEL_SMALL, seen[-26:]
+        for r in range(3):  # alternating batch by batch: always exact
+            run(tj, (jb, jo, jl), f"alternate jumbo {r}")
+            run(ts, (sb, so, sl), f"alternate short {r}")
+    finally:
+        e.close()
+
+
+def test_variant8_leaves_small_kernel_on_jumbo_frames():
+    """with variant 8 a batch of jumbo frames runs the small-frame kernel only
+    until its long report arrives; the launches after it run the 4-lane kernels, within 2x of the
+    automatic choice, and short traffic brings the small-frame kernel back. Bit-exact throughout."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    jb, jo, jl = synth.uniform_batch(8192, 9000, seed=23)
+    sb, so, sl = synth.hello_batch(4096, seed=24)
+    tj, ts = _dev_batch(jb, jo, jl), _dev_batch(sb, so, sl)
+
+    def timed(e, k=10):
+        out, st = e.digest_device(*tj)
+        torch.cuda.synchronize()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(k):
+            out, st = e.digest_device(*tj)
+        t1.record()
+        torch.cuda.synchronize()
+        return t0.elapsed_time(t1) / k, out, st
+
+    e8, e0 = Engine(0), Engine(0)
+    try:
+        e8.set_kernel(8)
+        out, st = e8.digest_device(*tj)  # the first launch: the small-frame kernel (no report yet)
+        torch.cuda.synchronize()
+        assert e8.last_kernel() == Engine.KERNEL_SMALL
+        _exact(out, st, jb, jo, jl, "variant 8, first jumbo launch")
+        ms8, out, st = timed(e8)
+        assert e8.last_kernel() in (Engine.KERNEL_MIXED, Engine.KERNEL_ONE_PASS)
+        _exact(out, st, jb, jo, jl, "variant 8 after the long report")
+        for _ in range(20):
+            timed(e0, 1)  # past variant 0's initial window
+        ms0, _, _ = timed(e0)
+        assert ms8 <= 2.0 * ms0, (ms8, ms0)
+        for _ in range(4):
+            out, st = e8.digest_device(*ts)
+            torch.cuda.synchronize()
+        assert e8.last_kernel() == Engine.KERNEL_SMALL
+        _exact(out, st, sb, so, sl, "variant 8, short again")
+    finally:
+        e8.close()
+        e0.close()

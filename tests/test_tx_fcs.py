@@ -12,6 +12,8 @@ import random
 import numpy as np
 import pytest
 
+import engines  # noqa: E402
+
 from oracle import coracle, pyref
 from seqs_amd import FCS_APPEND, FILL_CSUM, FS_ERR_FCS, synth
 
@@ -105,15 +107,12 @@ def _dev(x, torch):
     return torch.from_numpy(np.ascontiguousarray(x)).to("cuda:0")
 
 
-@pytest.fixture(scope="module", params=[4, 2, 0, 8], ids=["one_pass", "mixed", "auto", "small"])
+@pytest.fixture(scope="module", params=engines.VARIANTS, ids=engines.IDS)
 def engine(request):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from seqs_amd import Engine
-
-    e = Engine(0)
-    e.set_kernel(request.param)
+    e = engines.engine_for(request.param)
     yield e
     e.close()
 
