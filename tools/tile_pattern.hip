@@ -237,6 +237,114 @@ __global__ void __launch_bounds__(64 * WPB) k_stream(const u32x4* __restrict__ p
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// `span`: the contiguous-span decomposition with its compute skeleton. A
+// wave owns 64 consecutive frames (a contiguous span of the packed batch; per-frame work would then
+// be shared by 64 frames per instruction). Phase 1 streams the span as 1-KB rows (64 lanes x 16 B,
+// the plain-stream pattern) through a ring of PF rows; per row each lane folds its 16 B with 3
+// dependent Z4 lookups (U = Z4(Z4(Z4(d0)^d1)^d2)^d3), the 4 lanes of a 64-B block combine by a
+// 2-round tree (Z16 across lane pairs, Z32 across the pairs, by DPP) and lane 3 stores the block's
+// (value, sum) partial; phase 2, one lane per frame, loads its ~25 block partials and folds them
+// with dependent Z64 steps. Tables: the digest kernel's conflict-free replicated layout (256 B per
+// entry, 8 copies per byte table, a lane-dependent copy), Z4 + Z16 in the two halves of one 64-KB
+// region, Z32 + Z64 in another: 128 KB, so one workgroup of WPB waves per CU (C2's 65,536 frames
+// are 1,024 spans: 4 waves per CU). Partials go to a global scratch (L2-resident: 12 KB per wave).
+// The tables hold no CRC values and the result is not checked: this measures the read pattern with
+// the lookup / VALU / LDS / partial-store work of the decomposition, against the 4-lane kernel.
+__device__ __forceinline__ uint32_t span_xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+template <uint32_t kOff>
+__device__ __forceinline__ uint32_t span_z(const char* lds, uint32_t a, uint32_t cvec, const uint32_t (&sel)[4], uint32_t w) {
+    const uint32_t t0 = *reinterpret_cast<const uint32_t*>(lds + kOff + __builtin_amdgcn_perm(a, cvec, sel[0]));
+    const uint32_t t1 = *reinterpret_cast<const uint32_t*>(lds + kOff + __builtin_amdgcn_perm(a, cvec, sel[1]));
+    const uint32_t t2 = *reinterpret_cast<const uint32_t*>(lds + kOff + __builtin_amdgcn_perm(a, cvec, sel[2]));
+    const uint32_t t3 = *reinterpret_cast<const uint32_t*>(lds + kOff + __builtin_amdgcn_perm(a, cvec, sel[3]));
+    return span_xor3(span_xor3(t0, t1, t2), t3, w);
+}
+template <int PF, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_span(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
+                                                   uint2* __restrict__ part, uint32_t* out) {
+    __shared__ __attribute__((aligned(16))) char lds[131072];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    // tables: every thread writes 128 B (two regions x 256 entries x 256 B / (64 WPB threads))
+    for (uint32_t o = threadIdx.x * 16u; o < 131072u; o += 64u * WPB * 16u)
+        *reinterpret_cast<u32x4*>(lds + o) = u32x4{o * 0x9E3779B1u, o ^ 0x5bd1e995u, o * 7u, ~o};
+    __syncthreads();
+    uint32_t cvec = 0, sel[4];
+    {
+        const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) cvec |= (32u * j + 4u * c) << (8u * j);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t b = (k + h) & 3u;
+            sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
+        }
+    }
+    const uint32_t span = blockIdx.x * WPB + wave;
+    const uint32_t f0 = span * 64u;
+    if (f0 >= nframes) return;
+    const uint32_t nf = min(64u, nframes - f0);
+    const uint64_t s0 = (uint64_t)f0 * flen, s1 = (uint64_t)(f0 + nf) * flen;
+    const uint64_t b0 = s0 & ~uint64_t(63), bytes = ((s1 + 63) & ~uint64_t(63)) - b0;  // whole 64-B blocks
+    const int rows = (int)((bytes + 1023) / 1024);
+    const u32x4* rp = reinterpret_cast<const u32x4*>(base + b0) + lane;
+    const uint32_t nblk = (uint32_t)(bytes / 64);
+    uint2* wpart = part + (size_t)span * 2048u;
+    uint32_t acc = 0;
+    // phase 1
+    u32x4 pf[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) pf[i] = rp[64 * min(i, rows - 1)];
+    for (int r0 = 0; r0 < rows; r0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int r = r0 + i;
+            const u32x4 v = pf[i];
+            pf[i] = rp[64 * min(r + PF, rows - 1)];
+            // lane fold: 3 dependent Z4 rounds (region 0, low half)
+            uint32_t u = span_z<0>(lds, v.x, cvec, sel, v.y);
+            u = span_z<0>(lds, u, cvec, sel, v.z);
+            u = span_z<0>(lds, u, cvec, sel, v.w);
+            uint32_t cs = __builtin_amdgcn_sad_u16(v.x, 0u, 0u);
+            cs = __builtin_amdgcn_sad_u16(v.y, 0u, cs);
+            cs = __builtin_amdgcn_sad_u16(v.z, 0u, cs);
+            cs = __builtin_amdgcn_sad_u16(v.w, 0u, cs);
+            // block tree: Z16 across lane pairs (region 0, high half), Z32 across the pairs (region 1)
+            const uint32_t t = span_z<128>(lds, u, cvec, sel, 0u);
+            const uint32_t pr = u ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0xA0, 0xf, 0xf, false);  // [0,0,2,2]
+            const uint32_t q = span_z<65536>(lds, pr, cvec, sel, 0u);
+            const uint32_t y = pr ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0x55, 0xf, 0xf, false);  // [1,1,1,1]
+            cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0xB1, 0xf, 0xf, false);
+            cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0x4E, 0xf, 0xf, false);
+            const uint32_t blk = (uint32_t)r * 16u + (lane >> 2);
+            if ((lane & 3u) == 3u && blk < nblk) wpart[blk] = make_uint2(y, cs);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // phase 2: one lane per frame folds its blocks (dependent Z64 steps, region 1 high half)
+    if (lane < nf) {
+        const uint64_t fs = (uint64_t)(f0 + lane) * flen, fe = fs + flen;
+        const uint32_t k0 = (uint32_t)((fs - b0) / 64), k1 = (uint32_t)((fe - 1 - b0) / 64);
+        uint32_t y = 0, sum = 0;
+        for (uint32_t k = k0; k <= k1; k += 8) {
+            uint2 pv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pv[j] = wpart[min(k + j, k1)];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (k + j <= k1) {
+                    y = span_z<65536 + 128>(lds, y, cvec, sel, pv[j].x);
+                    sum += pv[j].y;
+                }
+        }
+        acc = y ^ sum;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     // `dir [flen]`: forward-only (AL 2) against alternating-direction (AL 3) whole blocks
     const bool dir = argc > 1 && std::string(argv[1]).rfind("dir", 0) == 0;
@@ -340,6 +448,24 @@ int main(int argc, char** argv) {
             TILESM(16, 6, 0, 1);
             TILESM(16, 5, 0, 0);
             TILESM(16, 5, 0, 1);
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "span") {
+        uint2* part;
+        const uint32_t nspans = (nf + 63) / 64;
+        CHECK(hipMalloc(&part, (size_t)nspans * 2048 * sizeof(uint2)));
+#define SPAN(PF, WPB)                                                                                      \
+    run([&](int i, hipStream_t s) {                                                                       \
+        hipLaunchKernelGGL((k_span<PF, WPB>), dim3((nspans + WPB - 1) / WPB), dim3(64 * WPB), 0, s, bufs[i % NB], nf, \
+                           flen, part, out);                                                              \
+    }, "span PF=" #PF " waves/WG=" #WPB)
+        for (int rep = 0; rep < 2; ++rep) {
+            STREAM(4, 16, 1);
+            TILES(4, 5, 2, 16);
+            SPAN(8, 4);
+            SPAN(12, 4);
+            SPAN(16, 4);
         }
         return 0;
     }
