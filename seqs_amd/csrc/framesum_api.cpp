@@ -434,6 +434,36 @@ static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames
     return FS_SUCCESS;
 }
 
+// A host-staged batch read in place: frames, offsets and lengths in pinned host memory the device
+// addresses directly (mapped), results written to host memory by the kernel (the caller's arrays when
+// pinned, else the mirror). The small-frame kernel only: its lanes read whole 16-B chunks of adjacent
+// frames, which the memory system turns into full-line PCIe reads.
+static fs_status host_inplace(fs_ctx* ctx, const uint8_t* d_frames, const uint64_t* d_off, const uint32_t* d_len,
+                              uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status) {
+    fs_status st = ensure_pinned(ctx, n);
+    if (st != FS_SUCCESS) return st;
+    void* d_out = mapped(out);
+    void* d_st = status ? mapped(status) : nullptr;
+    const bool direct = d_out && (!status || d_st);
+    if (!direct) {
+        d_out = ctx->d_pin + (size_t)n * 12;
+        d_st = status ? ctx->d_pin + (size_t)n * 20 : nullptr;
+    }
+    ctx->host_dirty = true;
+    const hipStream_t ks = ctx->compute_stream;
+    FS_HIP(ctx, launch(ctx, d_frames, d_off, d_len, n, mtu, reinterpret_cast<fs_digest*>(d_out),
+                       reinterpret_cast<uint8_t*>(d_st), ks, framesum::FsOp::kDigest, nullptr, 0,
+                       framesum::kForceSmallExact));
+    FS_HIP(ctx, hipEventRecord(ctx->host_done, ks));
+    FS_HIP(ctx, host_wait(ctx->host_done));
+    if (!direct) {
+        std::memcpy(out, ctx->h_pin + (size_t)n * 12, (size_t)n * sizeof(fs_digest));
+        if (status) std::memcpy(status, ctx->h_pin + (size_t)n * 20, n);
+    }
+    ctx->host_dirty = false;
+    return FS_SUCCESS;
+}
+
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status) {
     if (!ctx) return FS_E_INVALID;
@@ -445,6 +475,24 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     FS_HIP(ctx, hipSetDevice(ctx->device));
     fs_status pst = quiesce_host_streams(ctx);
     if (pst != FS_SUCCESS) return pst;
+    if (n <= kChunkFrames && ctx->force_kernel != 2 && ctx->force_kernel != 4) {
+        // A batch of short frames whose frames, offsets and lengths are all in pinned host memory:
+        // the small-frame kernel reads them in place over PCIe and writes its results to host
+        // memory, so the call is one launch -- no copies, no gaps between DMA commands.
+        const void* df = mapped(const_cast<uint8_t*>(frames));
+        const void* dof = df ? mapped(const_cast<uint64_t*>(offsets)) : nullptr;
+        const void* dln = dof ? mapped(const_cast<uint32_t*>(lengths)) : nullptr;
+        if (dln) {
+            const framesum::plan::Scan sc =
+                framesum::plan::scan_from(scan_descriptors(offsets, lengths, n), offsets, lengths, n, frames_bytes);
+            if (sc.bad < n)
+                return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
+            if (host_force(ctx, sc.max_len) == framesum::kForceSmallExact &&
+                (reinterpret_cast<uintptr_t>(df) & 3u) == 0u)
+                return host_inplace(ctx, static_cast<const uint8_t*>(df), static_cast<const uint64_t*>(dof),
+                                    static_cast<const uint32_t*>(dln), n, mtu, out, status);
+        }
+    }
     if (n <= kChunkFrames) {
         // The descriptors go to the device first, while the host scans them (they are n elements
         // of the caller's arrays whatever the scan finds; a frame out of range fails the call before

@@ -631,3 +631,41 @@ def test_variant8_leaves_small_kernel_on_jumbo_frames():
     finally:
         e8.close()
         e0.close()
+
+
+@pytest.mark.parametrize("pinned_results", [False, True])
+def test_host_small_batch_read_in_place(pinned_results):
+    """fs_digest_batch_host with frames, offsets and lengths all in pinned host memory and every
+    frame <= 128 B: the small-frame kernel reads them in place over PCIe (no staging copies) and
+    writes the results to host memory (into the caller's arrays when they are pinned). Bit-exact
+    against the oracle, including frames at odd offsets and a frames base at 16k + 4."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from seqs_amd.framesum import DIGEST_DTYPE
+
+    e = Engine(0)
+    try:
+        import framegen
+        frames = [f for f in framegen.edge_batch(41, n_random=3000) if len(f) <= 128]
+        buf, off, ln = pack_frames(frames, align=1)
+        assert int(ln.max()) <= 128 and len(ln) > 1000
+        n = len(ln)
+        pin = e.host_empty((len(buf) + 4,), np.uint8)
+        view = pin[4:]  # a base at 16k + 4
+        view[:] = buf
+        desc = e.host_empty((12 * n,), np.uint8)
+        poff, plen = desc[: 8 * n].view(np.uint64), desc[8 * n:].view(np.uint32)
+        poff[:] = off
+        plen[:] = ln
+        if pinned_results:
+            out, st = e.host_empty((n,), DIGEST_DTYPE), e.host_empty((n,), np.uint8)
+        else:
+            out, st = np.zeros(n, DIGEST_DTYPE), np.zeros(n, np.uint8)
+        for mtu in (0, 1514):
+            e.digest_host(view, poff, plen, mtu=mtu, out=out, status=st)
+            assert e.last_kernel() == Engine.KERNEL_SMALL
+            dig, est = coracle.digest_batch(buf, off, ln, mtu=mtu, nthreads=8)
+            assert np.array_equal(out["crc32"], dig["crc32"]) and np.array_equal(out["ip_csum"], dig["ip_csum"])
+            assert np.array_equal(out["l4_csum"], dig["l4_csum"]) and np.array_equal(st, est)
+    finally:
+        e.close()
