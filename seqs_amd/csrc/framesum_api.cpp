@@ -170,6 +170,24 @@ fs_status quiesce_host_streams(fs_ctx* ctx) {
     return FS_SUCCESS;
 }
 
+// A host-staged call that fails after it has enqueued work drains the context's streams before it
+// returns (best effort), so that nothing of it still reads the caller's buffers or writes the
+// caller's result arrays (the kernel writes them in place when they are pinned) after the error.
+void drain_host_streams(fs_ctx* ctx) {
+    const bool ok = hipStreamSynchronize(ctx->compute_stream) == hipSuccess &&
+                    hipStreamSynchronize(ctx->copy_stream) == hipSuccess &&
+                    hipStreamSynchronize(ctx->copy_stream2) == hipSuccess;
+    if (ok) ctx->host_dirty = false;
+}
+#define FS_HIP_DRAIN(ctx, call)                  \
+    do {                                         \
+        hipError_t e_ = (call);                  \
+        if (e_ != hipSuccess) {                  \
+            drain_host_streams(ctx);             \
+            return hip_err(ctx, e_, #call);      \
+        }                                        \
+    } while (0)
+
 // Wait on the host for `ev` by polling: HIP's blocking wait wakes the host about 25 us after the
 // work ends, a third of a short host-staged call. After 2 ms of polling (a long
 // batch) it falls back to the blocking wait instead of burning the core.
@@ -415,17 +433,20 @@ static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames
     const hipStream_t ks = ctx->compute_stream;
     // the frames behind the descriptors (issued by the caller before the scan), then the kernel, in
     // the compute stream's order: no cross-stream event between them
-    FS_HIP(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, ks));
-    if (ctx->fault_chunk == 0) return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: injected failure (test hook)");
+    FS_HIP_DRAIN(ctx, hipMemcpyAsync(sl.d_frames, frames + cpy_lo, cpy_hi - cpy_lo, hipMemcpyHostToDevice, ks));
+    if (ctx->fault_chunk == 0) {
+        drain_host_streams(ctx);
+        return set_err(ctx, FS_E_NOMEM, "fs_digest_batch_host: injected failure (test hook)");
+    }
     const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(sl.d_frames) - cpy_lo);
     const uint64_t* d_off = reinterpret_cast<const uint64_t*>(ctx->d_desc);
     const uint32_t* d_len = reinterpret_cast<const uint32_t*>(ctx->d_desc + (size_t)n * 8);
-    FS_HIP(ctx, launch(ctx, base, d_off, d_len, n, mtu, reinterpret_cast<fs_digest*>(d_out),
+    FS_HIP_DRAIN(ctx, launch(ctx, base, d_off, d_len, n, mtu, reinterpret_cast<fs_digest*>(d_out),
                        reinterpret_cast<uint8_t*>(d_st), ks, framesum::FsOp::kDigest, nullptr, 0, force));
-    FS_HIP(ctx, hipEventRecord(sl.consumed, ks));
+    FS_HIP_DRAIN(ctx, hipEventRecord(sl.consumed, ks));
     sl.used = true;
-    FS_HIP(ctx, hipEventRecord(ctx->host_done, ks));
-    FS_HIP(ctx, host_wait(ctx->host_done));
+    FS_HIP_DRAIN(ctx, hipEventRecord(ctx->host_done, ks));
+    FS_HIP_DRAIN(ctx, host_wait(ctx->host_done));
     if (!direct) {
         std::memcpy(out, ctx->h_pin + (size_t)n * 12, (size_t)n * sizeof(fs_digest));
         if (status) std::memcpy(status, ctx->h_pin + (size_t)n * 20, n);
@@ -451,11 +472,11 @@ static fs_status host_inplace(fs_ctx* ctx, const uint8_t* d_frames, const uint64
     }
     ctx->host_dirty = true;
     const hipStream_t ks = ctx->compute_stream;
-    FS_HIP(ctx, launch(ctx, d_frames, d_off, d_len, n, mtu, reinterpret_cast<fs_digest*>(d_out),
+    FS_HIP_DRAIN(ctx, launch(ctx, d_frames, d_off, d_len, n, mtu, reinterpret_cast<fs_digest*>(d_out),
                        reinterpret_cast<uint8_t*>(d_st), ks, framesum::FsOp::kDigest, nullptr, 0,
                        framesum::kForceSmallExact));
-    FS_HIP(ctx, hipEventRecord(ctx->host_done, ks));
-    FS_HIP(ctx, host_wait(ctx->host_done));
+    FS_HIP_DRAIN(ctx, hipEventRecord(ctx->host_done, ks));
+    FS_HIP_DRAIN(ctx, host_wait(ctx->host_done));
     if (!direct) {
         std::memcpy(out, ctx->h_pin + (size_t)n * 12, (size_t)n * sizeof(fs_digest));
         if (status) std::memcpy(status, ctx->h_pin + (size_t)n * 20, n);
@@ -514,16 +535,15 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         }
         const hipStream_t ks = ctx->compute_stream;
         if (reinterpret_cast<const uint8_t*>(src_off) + (size_t)n * 8 == reinterpret_cast<const uint8_t*>(src_len)) {
-            FS_HIP(ctx, hipMemcpyAsync(ctx->d_desc, src_off, (size_t)n * 12, hipMemcpyHostToDevice, ks));
+            FS_HIP_DRAIN(ctx, hipMemcpyAsync(ctx->d_desc, src_off, (size_t)n * 12, hipMemcpyHostToDevice, ks));
         } else {
-            FS_HIP(ctx, hipMemcpyAsync(ctx->d_desc, src_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
-            FS_HIP(ctx, hipMemcpyAsync(ctx->d_desc + (size_t)n * 8, src_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
+            FS_HIP_DRAIN(ctx, hipMemcpyAsync(ctx->d_desc, src_off, (size_t)n * 8, hipMemcpyHostToDevice, ks));
+            FS_HIP_DRAIN(ctx, hipMemcpyAsync(ctx->d_desc + (size_t)n * 8, src_len, (size_t)n * 4, hipMemcpyHostToDevice, ks));
         }
         const framesum::plan::Scan sc =
             framesum::plan::scan_from(scan_descriptors(offsets, lengths, n), offsets, lengths, n, frames_bytes);
         if (sc.bad < n) {
-            (void)hipStreamSynchronize(ks);  // the descriptor copy reads the caller's arrays: done before returning
-            ctx->host_dirty = false;
+            drain_host_streams(ctx);  // the descriptor copy reads the caller's arrays: done before returning
             return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
         }
         const int force = host_force(ctx, sc.max_len);
