@@ -1143,8 +1143,9 @@ __device__ __forceinline__ uint32_t tile_long(uint32_t len) {
     return group_max((int)min(len, 0x7fffffffu)) > (int)kSmallMaxLen ? kFlagLong : 0u;
 }
 
-// After the preamble barrier: wave 0 posts its workgroup's first-tile flags (one store per flag that
-// is set; the first workgroup then posts that the launch ran, after its own long flag).
+// Wave 0 posts its workgroup's first-tile flags, parked in LDS by every wave before the preamble
+// barrier (one store per flag that is set; the first workgroup then posts that the launch ran, after
+// its own long flag).
 __device__ __forceinline__ void post_workgroup(const char* lds, uint64_t report, uint32_t wave, uint32_t lane) {
     if (!report || wave != 0u || lane != 0u) return;
     uint32_t f = 0;
@@ -1264,7 +1265,6 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     else __builtin_amdgcn_s_waitcnt(0x0070);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
-    post_workgroup(lds, report, __builtin_amdgcn_readfirstlane(wave), lane);
     // two-level age priority: the SIMD's younger half (waves 8..15) outranks the older (round 2:
     // -0.35..-0.55 us per launch)
     if ((__builtin_amdgcn_readfirstlane(wave) >> 3) != 0u) __builtin_amdgcn_s_setprio(1);
@@ -1429,6 +1429,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             tile_header(T);
         }
     }
+    // the workgroup's first-tile flags, posted by wave 0 after its own work: a store to host memory
+    // counts in vmcnt until it lands (~PCIe latency), so posting it before the row loop held back
+    // that wave's counted waits (C2 +0.2 us per launch)
+    post_workgroup(lds, report, __builtin_amdgcn_readfirstlane(wave), lane);
 }
 
 // The kernel for batches with mixed lengths: tiles in mode A or mode B, per tile.
@@ -1500,7 +1504,6 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     tables_landed<kPrefetch>(first, U.P > 0, x4);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
-    post_workgroup(lds, report, wave, lane);
     if ((wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // two-level age priority: the SIMD's younger half first
     FS_STAMP(1);
 
@@ -1656,6 +1659,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             }
         }
     }
+    post_workgroup(lds, report, wave, lane);  // (after the wave's own work: see digest_kernel_a)
 }
 
 

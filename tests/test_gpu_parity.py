@@ -647,8 +647,10 @@ def test_host_small_batch_read_in_place(pinned_results):
     try:
         import framegen
         frames = [f for f in framegen.edge_batch(41, n_random=3000) if len(f) <= 128]
+        hb, ho, hl = synth.hello_batch(3000, seed=42)
+        frames += [bytes(hb[int(o):int(o) + int(l)]) for o, l in zip(ho, hl)]
         buf, off, ln = pack_frames(frames, align=1)
-        assert int(ln.max()) <= 128 and len(ln) > 1000
+        assert int(ln.max()) <= 128 and len(ln) > 3000
         n = len(ln)
         pin = e.host_empty((len(buf) + 4,), np.uint8)
         view = pin[4:]  # a base at 16k + 4
