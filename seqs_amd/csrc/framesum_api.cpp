@@ -284,7 +284,7 @@ fs_status fs_ctx_create(int device, fs_ctx** out) {
             ctx->h_report[framesum::kReportSeen] = 0u;
             ctx->h_report[framesum::kReportSeenSeq] = 0u;
             for (int w : {framesum::kReportLong, framesum::kReportRan, framesum::kReportLongSeen,
-                          framesum::kReportRanSeen, framesum::kReportShort})
+                          framesum::kReportRanSeen, framesum::kReportShort, framesum::kReportLongEver})
                 ctx->h_report[w] = 0u;
             e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_report), hp, 0);
         }

@@ -61,14 +61,25 @@ constexpr uint32_t kInitialMixedLaunches = 16;
 // The short-frame choice (the small-frame kernel, variant 8, for traffic of frames <= kSmallMaxLen
 // bytes): kReportLong and kReportRan are written by the device -- the latest launch
 // id that met a frame longer than kSmallMaxLen, and the latest launch id that ran a 4-lane kernel
-// (its first workgroup, after that workgroup has posted its own long flag); kReportLongSeen,
-// kReportRanSeen and kReportShort only by the host: the two words as it last saw them and the
-// number of launches seen to run since the latest long report (launch_digest).
+// (posted by the grid's first wave, with kReportRanLong set when its own tile held such a frame);
+// kReportLongSeen, kReportRanSeen, kReportShort and kReportLongEver only by the host: the two words
+// as it last saw them, the number of launches seen to run since the latest long report, and whether
+// any long report has arrived (launch_digest).
 constexpr int kReportLong = 5, kReportRan = 6, kReportLongSeen = 7, kReportRanSeen = 8, kReportShort = 9;
+constexpr int kReportLongEver = 10;
+constexpr uint32_t kReportRanLong = 1u << 16;
 constexpr uint32_t kSmallMaxLen = 128;
-// the kernels' `report` argument: the report block's device address in bits 0..46 (host-mapped
-// memory sits below 2^47), a watch flag in bit 47, the launch id in bits 48..63
-constexpr uint64_t kReportAddrMask = (1ull << 47) - 1u;
+// the kernels' `report` argument: the report block's device address in bits 6..46 (host-mapped
+// memory sits below 2^47; the block is 64-B aligned), a watch flag in bit 47, the launch id in bits
+// 48..63, and in bits 0..1 what this launch is asked to post: kAskRan (the grid's first tile posts
+// kReportRan) and kAskMixed (the mixed-length kernel posts its mixed tiles; the one-pass kernel
+// always does). Each post costs the launch ~0.28 us (C2), so steady traffic is sampled: "ran" on
+// every kRanSample-th launch under variant 0 (every launch while the host counts short launches,
+// and every launch under variant 8), "mixed" from the
+// mixed-length kernel on every kMixedSample-th launch (and until the first report).
+constexpr uint64_t kReportAddrMask = ((1ull << 47) - 1u) & ~63ull;
+constexpr uint64_t kAskRan = 1u, kAskMixed = 2u;
+constexpr uint32_t kRanSample = 4, kMixedSample = 32;
 // launches seen to run without a long frame before variant 0 moves to the small-frame kernel, and
 // before a variant-8 context that met long frames goes back to it
 constexpr uint32_t kShortLaunchesAuto = 16, kShortLaunchesSmall = 2;

@@ -102,11 +102,7 @@ static_assert(kTablesLdsBytes == kLdsTables, "FsTables is the LDS image of the t
 
 // The workgroup's LDS image (static allocation of the digest kernels). Namespace scope, so the
 // out-of-line parse routine addresses it as LDS (ds_read), not through a flat pointer.
-// Per-wave report flags of a workgroup's first tiles (bit 0: a frame longer than kSmallMaxLen; bit 1:
-// a tile worth mode B), read by wave 0 after the preamble barrier: one post per workgroup.
-constexpr uint32_t kLdsFlags = kLdsBytes;
-constexpr uint32_t kFlagLong = 1u, kFlagMixed = 2u;
-__shared__ __attribute__((aligned(16))) char g_lds[kLdsBytes + 4 * kWavesPerBlock];
+__shared__ __attribute__((aligned(16))) char g_lds[kLdsBytes];
 
 #ifdef FS_STAMPS
 // Diagnostic build only: per-wave s_memtime phase stamps, read back by fs_debug_read_stamps().
@@ -1125,38 +1121,47 @@ struct LayA1 : LayoutA {
 // id in bits 48..63
 // (one kernel argument, loaded where it is used: nothing of it stays live through the tile loop).
 template <int kWord = kReportLatest>
-__device__ __forceinline__ void post_report(uint64_t report) {
+__device__ __forceinline__ void post_report(uint64_t report, uint32_t bits = 0u) {
     asm volatile("" : "+s"(report));  // split here, not hoisted into a register held by the whole kernel
     // a GLOBAL store (address space 1), not a flat one: hipcc's wait counting treats any pending
     // flat op as able to complete out of order with the vector memory operations, so every vmcnt
     // wait after it became vmcnt(0) -- the first block of rows waited for the whole ring
     typedef __attribute__((address_space(1))) uint32_t gu32;
-    *reinterpret_cast<gu32*>((report & kReportAddrMask) + 4u * kWord) = (uint32_t)(report >> 48);
+    *reinterpret_cast<gu32*>((report & kReportAddrMask) + 4u * kWord) = (uint32_t)(report >> 48) | bits;
 }
 // Bit 47 of `report`: the host is counting short launches (or a long report is news to it), so every
-// workgroup reports its long frames; otherwise only the first workgroup does, beside its "ran" post
-// (uniform long traffic then costs one post per launch, not one per workgroup).
+// wave reports its long tiles; otherwise only the grid's first wave does, in its "ran" post (uniform
+// long traffic then costs one post per launch, not one per tile).
 __device__ __forceinline__ bool report_watch(uint64_t report) { return ((report >> 47) & 1u) != 0u; }
 
-// A wave's report flags for its tile (frames of `len`, group-uniform; 0 for an empty group).
-__device__ __forceinline__ uint32_t tile_long(uint32_t len) {
-    return group_max((int)min(len, 0x7fffffffu)) > (int)kSmallMaxLen ? kFlagLong : 0u;
+// A wave's posts for a tile of frames of `len` (group-uniform; 0 for an empty group), issued at the
+// tile's start, after its row prefetch. A store to host memory counts in vmcnt until it lands (~PCIe
+// latency): a wait for any load issued after it waits for the store too. Each post costs its launch
+// about 0.25 us (C2: one store from the grid's first wave; placements tried, same box: at the first
+// tile's start +0.25 us, just before the tile's last block about the same but +18 VGPRs in the
+// one-pass kernel, after the wave's own work +0.27 us on C2 and +1.1 us on C3), hence the sampled
+// asks (kAskRan, kAskMixed). The grid's first tile posts "ran" with its own long flag in the same
+// word (kReportRanLong), so a launch it saw long never reads as short, whatever order posts land in.
+// What a tile posts (wave-uniform bits), computed apart from the stores so that a wave's first tile
+// computes them while its rows load and stores them after its counted wait (computing them after the
+// wait put the wave's barrier arrival ~0.1 us later on C2). kMixedOnAsk: mixed tiles are posted only
+// when the launch asks (kAskMixed; the mixed-length kernel).
+constexpr uint32_t kPostMixed = 1u, kPostRan = 2u, kPostRanLong = 4u, kPostLong = 8u;
+template <bool kMixedOnAsk>
+__device__ __forceinline__ uint32_t tile_posts(uint64_t report, uint32_t len, bool mixed_tile, bool first_tile_of_grid) {
+    // the bit tests here, per tile: hoisted out of the tile loop, hipcc kept each flag as a live
+    // 64-bit mask and spilled SGPRs (the mixed-length kernel 24 against 14, C3 +1.1 us per launch)
+    asm volatile("" : "+s"(report));
+    const bool mixed = mixed_tile && (!kMixedOnAsk || (report & kAskMixed) != 0u);
+    const bool ran = first_tile_of_grid && (report & kAskRan) != 0u;
+    const bool lng = (ran || report_watch(report)) && __ballot(len > kSmallMaxLen) != 0u;
+    return (mixed ? kPostMixed : 0u) | (ran ? (lng ? kPostRan | kPostRanLong : kPostRan) : (lng ? kPostLong : 0u));
 }
-
-// Wave 0 posts its workgroup's first-tile flags, parked in LDS by every wave before the preamble
-// barrier (one store per flag that is set; the first workgroup then posts that the launch ran, after
-// its own long flag).
-__device__ __forceinline__ void post_workgroup(const char* lds, uint64_t report, uint32_t wave, uint32_t lane) {
-    if (!report || wave != 0u || lane != 0u) return;
-    uint32_t f = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kWavesPerBlock; j += 4) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(lds + kLdsFlags + 4u * j);
-        f |= v.x | v.y | v.z | v.w;
-    }
-    if ((f & kFlagLong) && (blockIdx.x == 0u || report_watch(report))) post_report<kReportLong>(report);
-    if (f & kFlagMixed) post_report<kReportLatest>(report);
-    if (blockIdx.x == 0u) post_report<kReportRan>(report);
+__device__ __forceinline__ void post_tile(uint64_t report, uint32_t posts, uint32_t lane) {
+    if (posts == 0u || lane != 0u) return;
+    if (posts & kPostMixed) post_report<kReportLatest>(report);
+    if (posts & kPostRan) post_report<kReportRan>(report, (posts & kPostRanLong) ? kReportRanLong : 0u);
+    if (posts & kPostLong) post_report<kReportLong>(report);
 }
 // The wave's first tile (later tiles: + all waves): wave-major, so a workgroup's waves read tiles
 // spread over the batch and neighbouring workgroups (on different XCDs) neighbouring tiles.
@@ -1253,16 +1258,15 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         for (int i = 0; i < kPfA; ++i) pf[i] = load_row(T.gfb, lpos(T.rel0 + kRowDwords * i, T.lo));
     }
     if (first) tile_geometry_a_tail<Lay::kCapBlocks>(T);
-    // this wave's first-tile report flags, posted once per workgroup after the barrier
-    uint32_t wflags = 0u;
-    if (first && report) wflags = tile_long(T.len) | (mode_b_worthy(T.nd()) ? kFlagMixed : 0u);
-    if (lane == 0u) *reinterpret_cast<uint32_t*>(lds + kLdsFlags + 4u * wave) = wflags;
+    const uint32_t posts0 = first && report ? tile_posts<false>(report, T.len, mode_b_worthy(T.nd()), gwave == 0u) : 0u;
     if (first) tile_header(T);
     FS_STAMP(13);
     FS_STAMP(9);
     // the tables are this wave's own LDS stores: only the rows stay in flight
     if (first && T.P > 0) __builtin_amdgcn_s_waitcnt(0x0070 | kPfA);
     else __builtin_amdgcn_s_waitcnt(0x0070);
+    // (after the counted wait above, younger than the rows)
+    post_tile(report, posts0, lane);
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     // two-level age priority: the SIMD's younger half (waves 8..15) outranks the older (round 2:
@@ -1417,8 +1421,6 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
             tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
             descriptors_ready<kOps>(S, len);
             tile_geometry_a<Lay::kCapBlocks>(T, tile, grp, gl, n, S, len, frames, fpt);
-            if (report && mode_b_worthy(T.nd()) && lane == 0u) post_report(report);
-            if (report && report_watch(report) && tile_long(T.len) && lane == 0u) post_report<kReportLong>(report);
             if (T.P > 0) {
 #pragma unroll
                 for (int i = 0; i < kPfA; ++i) {
@@ -1426,13 +1428,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                     pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
                 }
             }
+            if (report) post_tile(report, tile_posts<false>(report, T.len, mode_b_worthy(T.nd()), false), lane);
             tile_header(T);
         }
     }
-    // the workgroup's first-tile flags, posted by wave 0 after its own work: a store to host memory
-    // counts in vmcnt until it lands (~PCIe latency), so posting it before the row loop held back
-    // that wave's counted waits (C2 +0.2 us per launch)
-    post_workgroup(lds, report, __builtin_amdgcn_readfirstlane(wave), lane);
 }
 
 // The kernel for batches with mixed lengths: tiles in mode A or mode B, per tile.
@@ -1496,12 +1495,10 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     // is all the parse's vmcnt(kPrefetch) needs)
     if (first) prefetch_unit(U, pf);
     if (first) x4 = header_dma<false>(T, frames, lds, hw, gl0, lane);
-    // this wave's first-tile report flags, posted once per workgroup after the barrier
-    uint32_t wflags = 0u;
-    if (first && report) wflags = tile_long(T.len) | (T.npass > 1 ? kFlagMixed : 0u);
-    if (lane == 0u) *reinterpret_cast<uint32_t*>(lds + kLdsFlags + 4u * wave) = wflags;
+    const uint32_t posts0 = first && report ? tile_posts<true>(report, T.len, T.npass > 1, gwave == 0u) : 0u;
     FS_STAMP(9);
     tables_landed<kPrefetch>(first, U.P > 0, x4);
+    post_tile(report, posts0, lane);  // (after the counted wait, younger than the rows)
     FS_STAMP(10);
     __builtin_amdgcn_s_barrier();  // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
     if ((wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // two-level age priority: the SIMD's younger half first
@@ -1569,7 +1566,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             using No = std::false_type;
             const int Rc = U.P - kPrefetch;  // first row of the last block
             if (U.P > 0) {
-                // [first block] (pass 0: parse) [head blocks: general] [body: lean] [last block]
+                // [first block] (pass 0: parse) [head blocks: general] [body: lean] post [last block]
                 if (Rc > 0) {
                     if (U.H > 0) block(0, Yes());
                     else lean_block(0, Yes());
@@ -1652,14 +1649,9 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             tile_geometry(T, U, tile, grp, gl, n, S, len, frames, lds, ws, fpt);
             header_dma<false>(T, frames, lds, hw, gl, lane);
             prefetch_unit(U, pf);
-            // a later tile of this wave (the first tiles' flags went out with the workgroup's post)
-            if (report) {
-                if (T.npass > 1 && lane == 0u) post_report(report);  // this launch met a mixed tile
-                if (report_watch(report) && tile_long(T.len) && lane == 0u) post_report<kReportLong>(report);
-            }
+            if (report) post_tile(report, tile_posts<true>(report, T.len, T.npass > 1, false), lane);
         }
     }
-    post_workgroup(lds, report, wave, lane);  // (after the wave's own work: see digest_kernel_a)
 }
 
 
@@ -1852,7 +1844,8 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     // The report of the launches before (the latest launch id that met a mixed-length tile):
     // launches are enqueued ahead of the GPU, so a report arrives several launches late; the
     // mixed kernel stays chosen for kStickyLaunches launches after the latest report (it keeps
-    // reporting while the traffic is mixed). A heuristic only: never a result.
+    // reporting while the traffic is mixed, on every kMixedSample-th launch). A heuristic only:
+    // never a result.
     // Launch ids are 16-bit (they travel in the report pointer's top bits; 0 = never reported).
     // The window is timed on the host instead: `next_id` is the context's 32-bit launch sequence,
     // and the host notes the sequence at which it first saw the report word change (host-only
@@ -1865,7 +1858,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     uint32_t id = seq & 0xFFFFu;
     if (id == 0u) id = 0x8000u;  // (0 means "never reported"; any non-zero tag will do)
     const uint64_t rdev = reinterpret_cast<uint64_t>(report_dev);
-    const bool can_report = report_host && rdev != 0u && (rdev & ~kReportAddrMask) == 0u;
+    const bool can_report = report_host && rdev != 0u && (rdev & ~kReportAddrMask) == 0u;  // (64-B aligned too)
     uint64_t report = can_report ? rdev | ((uint64_t)id << 48) : 0u;
     bool mixed = false;
     if (can_report) {
@@ -1875,6 +1868,8 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
             report_host[kReportSeenSeq] = seq;
         }
         mixed = latest != 0u && seq - report_host[kReportSeenSeq] <= kStickyLaunches;
+        // the mixed-length kernel's own posts only refresh the window: sampled (kMixedSample)
+        if (latest == 0u || seq % kMixedSample == 0u) report |= kAskMixed;
         // A context's first launches run the mixed-length kernel: it reports its own mode-B tiles,
         // so mixed traffic keeps it from the first batch on (the one-pass kernel's report would
         // arrive launches late, after slow first batches), and uniform traffic moves to the
@@ -1898,19 +1893,25 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     // path, which has seen every length.
     bool small = false;
     if (can_report) {
-        const uint32_t lng = report_host[kReportLong], ran = report_host[kReportRan];
-        if (lng != report_host[kReportLongSeen]) {
+        const uint32_t lng = report_host[kReportLong], rw = report_host[kReportRan], ran = rw & 0xFFFFu;
+        const bool ran_new = ran != report_host[kReportRanSeen];
+        if (lng != report_host[kReportLongSeen] || (ran_new && (rw & kReportRanLong) != 0u)) {
             report_host[kReportLongSeen] = lng;
             report_host[kReportShort] = 0u;
-        } else if (ran != report_host[kReportRanSeen] && ran != lng && report_host[kReportShort] < (1u << 30)) {
+            report_host[kReportLongEver] = 1u;
+        } else if (ran_new && ran != lng && report_host[kReportShort] < (1u << 30)) {
             report_host[kReportShort] = report_host[kReportShort] + 1u;
         }
         report_host[kReportRanSeen] = ran;
         const uint32_t streak = report_host[kReportShort];
         if (force == 0) small = streak >= kShortLaunchesAuto;
-        if (force == 8) small = lng == 0u || streak >= kShortLaunchesSmall;
+        if (force == 8) small = report_host[kReportLongEver] == 0u || streak >= kShortLaunchesSmall;
         // every workgroup reports its long frames while the host counts short launches
         if ((force == 0 || force == 8) && streak > 0u) report |= 1ull << 47;
+        // "ran": variant 0 samples it on long traffic and asks every launch while it counts short
+        // ones; variant 8 (short traffic expected: back to the small-frame kernel after 2 short
+        // launches) asks every launch
+        if (force == 8 || (force == 0 && (streak > 0u || seq % kRanSample == 0u))) report |= kAskRan;
     } else if (force == 8) {
         small = true;  // no report block: the caller's choice as it stands
     }

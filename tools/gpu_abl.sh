@@ -9,8 +9,10 @@ run() { local name=$1; shift; timeout -k 10 180 "$@" > $O/$name.json 2> $O/$name
 for rep in $(seq 1 ${REPS:-2}); do
   for v in "$@"; do
     L=$(lib $v)
-    FRAMESUM_LIB=$L run ${v}_c2_$rep python bench.py --steps 2000 --warmup 500 --cpu-seconds 0
-    FRAMESUM_LIB=$L run ${v}_c2k20_$rep python bench.py --steps 20 --warmup 5 --cpu-seconds 0
-    FRAMESUM_LIB=$L run ${v}_c3_$rep python bench.py --config c3 --steps 1000 --warmup 500 --cpu-seconds 0
+    for c in ${CFGS:-c2 c2k20 c3}; do case $c in
+      c2) FRAMESUM_LIB=$L run ${v}_c2_$rep python bench.py --steps 2000 --warmup 500 --cpu-seconds 0 ;;
+      c2k20) FRAMESUM_LIB=$L run ${v}_c2k20_$rep python bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
+      c3) FRAMESUM_LIB=$L run ${v}_c3_$rep python bench.py --config c3 --steps 1000 --warmup 500 --cpu-seconds 0 ;;
+    esac; done
   done
 done
