@@ -227,9 +227,10 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
  * batches of similar frame lengths (each frame read as the 64-byte blocks that hold it), a
  * mixed-length kernel that splits long frames into 768-byte pieces when a tile of 16 frames mixes
  * very different lengths, and a small-frame kernel (one lane per frame, small workgroups) for
- * traffic of short frames such as the reference's 47-byte benchmark frames. The kernels report,
- * per launch, whether its batch had mixed-length tiles and whether it had a frame longer than 128
- * bytes; the host reads those reports a few launches late.
+ * traffic of short frames such as the reference's 47-byte benchmark frames. The kernels report
+ * whether a launch's batch had mixed-length tiles and whether it had a frame longer than 128 bytes
+ * (sampled on steady traffic: each report is a store to host memory); the host reads those reports
+ * a few launches late.
  *   0 (default): automatic. Mixed-length tiles select the mixed-length kernel, similar lengths the
  *     one-pass kernel; after 16 launches seen to run with no frame over 128 bytes, the small-frame
  *     kernel, until a launch reports a longer frame.
