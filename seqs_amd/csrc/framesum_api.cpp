@@ -52,6 +52,9 @@ struct fs_ctx {
     // library's fs_test_set_fault (-DFS_TEST_HOOKS): fs_digest_batch_host fails with FS_E_NOMEM at
     // chunk k, after the earlier chunks' work and chunk k's copy are queued. -1 in the product.
     long fault_chunk = -1;
+    // the path the latest fs_digest_batch_host took (fs_test_last_host_path): 1 staged in one
+    // chunk, 2 read in place, 3 chunked
+    int last_host_path = 0;
     // host-mapped word the kernels set when a batch has widely mixed lengths (launch_digest)
     volatile uint32_t* h_report = nullptr;
     uint32_t* d_report = nullptr;
@@ -200,17 +203,28 @@ hipError_t host_wait(hipEvent_t ev) {
     }
 }
 
-// Is [p, p + bytes) page-locked host memory the GPU can copy from / to asynchronously (fs_host_alloc,
-// hipHostMalloc, hipHostRegister)? Then a host-staged call copies straight from / to it instead of
-// going through the context's pinned mirror (one host memcpy less per array).
-bool is_pinned(const void* p) {
+// Is [p, p + bytes) inside ONE page-locked host allocation the GPU can copy from / to asynchronously
+// (fs_host_alloc, hipHostMalloc, hipHostRegister)? Then a host-staged call copies straight from / to
+// it, or has the kernel read or write it in place, instead of going through the context's pinned
+// mirror. The whole span is checked, not only its start: a DMA or a kernel access past the end of a
+// pinned allocation would fault the GPU, where the mirror path's host memcpy stays on the host.
+bool is_pinned(const void* p, size_t bytes) {
     if (!p) return false;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();  // pageable memory: not an error of the call
         return false;
     }
-    return a.type == hipMemoryTypeHost;
+    if (a.type != hipMemoryTypeHost) return false;
+    void* start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, const_cast<void*>(p)) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, const_cast<void*>(p)) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;  // the span cannot be checked: take the mirror path
+    }
+    const uintptr_t b = reinterpret_cast<uintptr_t>(start), q = reinterpret_cast<uintptr_t>(p);
+    return q >= b && bytes <= size && q - b <= size - bytes;
 }
 
 // One launch of the context's kernel choice.
@@ -401,9 +415,10 @@ FS_HOST_CLONES static framesum::plan::ScanCore scan_descriptors(const uint64_t* 
 // the frames and one of the descriptors on the two copy streams at once, one launch, the results'
 // D2H, and a polled wait. Descriptors and results go straight from / to the caller's arrays when
 // those are pinned (fs_host_alloc), through the context's pinned mirror otherwise.
-// The device address of pinned host memory the kernel can write its results to directly, or null.
-static void* mapped(void* p) {
-    if (!p || !is_pinned(p)) return nullptr;
+// The device address of pinned host memory [p, p + bytes) the kernel can read or write directly, or
+// null.
+static void* mapped(void* p, size_t bytes) {
+    if (!p || !is_pinned(p, bytes)) return nullptr;
     void* d = nullptr;
     if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
         (void)hipGetLastError();
@@ -415,6 +430,7 @@ static void* mapped(void* p) {
 static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                              const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status,
                              const framesum::plan::Scan& sc, int force) {
+    ctx->last_host_path = 1;
     uint64_t cpy_lo, cpy_hi;
     framesum::plan::copy_span(sc.lo, sc.hi, frames_bytes, cpy_lo, cpy_hi);
     HostSlot& sl = ctx->slot[0];
@@ -423,8 +439,8 @@ static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames
     // The kernel writes the digests and verdicts straight to host memory (mapped pinned memory: no
     // D2H copy, no gap before it): into the caller's arrays when they are pinned, else into the
     // context's pinned mirror, copied out after the wait.
-    void* d_out = mapped(out);
-    void* d_st = status ? mapped(status) : nullptr;
+    void* d_out = mapped(out, (size_t)n * sizeof(fs_digest));
+    void* d_st = status ? mapped(status, n) : nullptr;
     const bool direct = d_out && (!status || d_st);
     if (!direct) {
         d_out = ctx->d_pin + (size_t)n * 12;
@@ -461,10 +477,11 @@ static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames
 // frames, which the memory system turns into full-line PCIe reads.
 static fs_status host_inplace(fs_ctx* ctx, const uint8_t* d_frames, const uint64_t* d_off, const uint32_t* d_len,
                               uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status) {
+    ctx->last_host_path = 2;
     fs_status st = ensure_pinned(ctx, n);
     if (st != FS_SUCCESS) return st;
-    void* d_out = mapped(out);
-    void* d_st = status ? mapped(status) : nullptr;
+    void* d_out = mapped(out, (size_t)n * sizeof(fs_digest));
+    void* d_st = status ? mapped(status, n) : nullptr;
     const bool direct = d_out && (!status || d_st);
     if (!direct) {
         d_out = ctx->d_pin + (size_t)n * 12;
@@ -500,17 +517,19 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         // A batch of short frames whose frames, offsets and lengths are all in pinned host memory:
         // the small-frame kernel reads them in place over PCIe and writes its results to host
         // memory, so the call is one launch -- no copies, no gaps between DMA commands.
-        const void* df = mapped(const_cast<uint8_t*>(frames));
-        const void* dof = df ? mapped(const_cast<uint64_t*>(offsets)) : nullptr;
-        const void* dln = dof ? mapped(const_cast<uint32_t*>(lengths)) : nullptr;
-        if (dln) {
+        // (the frames' span is checked once the scan has found it: the 16-B chunks the kernel reads
+        // stay in the pages that hold frame bytes, and pinned allocations are whole pages)
+        const void* dof = mapped(const_cast<uint64_t*>(offsets), (size_t)n * 8);
+        const void* dln = dof ? mapped(const_cast<uint32_t*>(lengths), (size_t)n * 4) : nullptr;
+        if (dln && is_pinned(frames, 1)) {
             const framesum::plan::Scan sc =
                 framesum::plan::scan_from(scan_descriptors(offsets, lengths, n), offsets, lengths, n, frames_bytes);
             if (sc.bad < n)
                 return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
-            if (host_force(ctx, sc.max_len) == framesum::kForceSmallExact &&
-                (reinterpret_cast<uintptr_t>(df) & 3u) == 0u)
-                return host_inplace(ctx, static_cast<const uint8_t*>(df), static_cast<const uint64_t*>(dof),
+            const void* df = sc.hi > sc.lo ? mapped(const_cast<uint8_t*>(frames + sc.lo), sc.hi - sc.lo) : nullptr;
+            if (df && host_force(ctx, sc.max_len) == framesum::kForceSmallExact &&
+                (reinterpret_cast<uintptr_t>(frames) & 3u) == 0u)
+                return host_inplace(ctx, static_cast<const uint8_t*>(df) - sc.lo, static_cast<const uint64_t*>(dof),
                                     static_cast<const uint32_t*>(dln), n, mtu, out, status);
         }
     }
@@ -524,7 +543,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         if (pst == FS_SUCCESS) pst = ensure_pinned(ctx, n);
         if (pst != FS_SUCCESS) return pst;
         ctx->host_dirty = true;  // until this call has waited for all of its work
-        const bool pin_desc = is_pinned(offsets) && is_pinned(lengths);
+        const bool pin_desc = is_pinned(offsets, (size_t)n * 8) && is_pinned(lengths, (size_t)n * 4);
         const uint64_t* src_off = offsets;
         const uint32_t* src_len = lengths;
         if (!pin_desc) {
@@ -557,6 +576,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
     const int force = host_force(ctx, sc.max_len);
     ctx->host_dirty = true;  // until this call has waited for all of its work
+    ctx->last_host_path = 3;
     pst = ensure_pinned(ctx, n);
     if (pst != FS_SUCCESS) return pst;
     pst = ensure_desc(ctx, n);
@@ -841,6 +861,9 @@ fs_status fs_test_set_kernel_exact(fs_ctx* ctx, int force) {
     ctx->force_kernel = force;
     return FS_SUCCESS;
 }
+// ... and which path the latest fs_digest_batch_host took: 1 staged in one chunk, 2 read in place,
+// 3 chunked (0 before the first call).
+int fs_test_last_host_path(const fs_ctx* ctx) { return ctx ? ctx->last_host_path : -1; }
 #endif
 
 fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out) {

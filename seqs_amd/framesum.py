@@ -170,6 +170,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         lib.fs_test_group_set_fault_gather.argtypes = [vp, ctypes.c_long]
         lib.fs_test_set_kernel_exact.restype = i32
         lib.fs_test_set_kernel_exact.argtypes = [vp, ctypes.c_int]
+        lib.fs_test_last_host_path.restype = ctypes.c_int
+        lib.fs_test_last_host_path.argtypes = [vp]
     _libs[p] = lib
     if path is None:
         _lib = lib

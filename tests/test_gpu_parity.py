@@ -643,7 +643,9 @@ def test_host_small_batch_read_in_place(pinned_results):
         pytest.skip("no GPU")
     from seqs_amd.framesum import DIGEST_DTYPE
 
-    e = Engine(0)
+    from seqs_amd.framesum import TEST_LIB_PATH
+
+    e = Engine(0, lib_path=TEST_LIB_PATH)
     try:
         import framegen
         frames = [f for f in framegen.edge_batch(41, n_random=3000) if len(f) <= 128]
@@ -663,11 +665,16 @@ def test_host_small_batch_read_in_place(pinned_results):
             out, st = e.host_empty((n,), DIGEST_DTYPE), e.host_empty((n,), np.uint8)
         else:
             out, st = np.zeros(n, DIGEST_DTYPE), np.zeros(n, np.uint8)
-        for mtu in (0, 1514):
-            e.digest_host(view, poff, plen, mtu=mtu, out=out, status=st)
-            assert e.last_kernel() == Engine.KERNEL_SMALL
-            dig, est = coracle.digest_batch(buf, off, ln, mtu=mtu, nthreads=8)
-            assert np.array_equal(out["crc32"], dig["crc32"]) and np.array_equal(out["ip_csum"], dig["ip_csum"])
-            assert np.array_equal(out["l4_csum"], dig["l4_csum"]) and np.array_equal(st, est)
+        # in place: every array pinned; staged (path 1): the same frames from pageable memory
+        for frames_arg, path in ((view, 2), (buf, 1)):
+            for mtu in (0, 1514):
+                out[:] = np.zeros(1, DIGEST_DTYPE)
+                st[:] = 0xFF
+                e.digest_host(frames_arg, poff, plen, mtu=mtu, out=out, status=st)
+                assert e.last_kernel() == Engine.KERNEL_SMALL
+                assert e.lib.fs_test_last_host_path(e._ctx) == path
+                dig, est = coracle.digest_batch(buf, off, ln, mtu=mtu, nthreads=8)
+                assert np.array_equal(out["crc32"], dig["crc32"]) and np.array_equal(out["ip_csum"], dig["ip_csum"])
+                assert np.array_equal(out["l4_csum"], dig["l4_csum"]) and np.array_equal(st, est)
     finally:
         e.close()
