@@ -62,7 +62,7 @@ for step in "$@"; do
     timeout -k 10 1000 bash tools/gpu_abl.sh ${arg//,/ } || exit 1 ;;
   pmc)
     IFS=: read -r tag k cfg <<< "$arg"
-    CFG=${cfg:-c2} timeout -k 10 600 bash tools/gpu_r3_pmc.sh $tag $k || exit 1 ;;
+    CFG=${cfg:-c2} timeout -k 10 600 bash tools/gpu_pmc_variant.sh $tag $k || exit 1 ;;
   py)
     timeout -k 10 600 python3 $arg > $O/py_$i.log 2>&1 || { echo "FAIL py $arg"; tail -10 $O/py_$i.log; exit 1; }
     tail -20 $O/py_$i.log ;;

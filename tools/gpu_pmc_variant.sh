@@ -1,5 +1,5 @@
 # Round 3: PMC passes (kernel trace only) + a kernel trace for kernel variants on C2.
-# usage: tools/gpu_r3_pmc.sh <tag> <kernel> [<tag> <kernel> ...]   (FS_RX_GRID passes through)
+# usage: tools/gpu_pmc_variant.sh <tag> <kernel> [<tag> <kernel> ...]   (FS_RX_GRID passes through)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
 O="$R/gpurun_out/r3pmc"; mkdir -p "$O"
