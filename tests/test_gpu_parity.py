@@ -588,6 +588,35 @@ def test_auto_choice_short_frames_device():
         e.close()
 
 
+def test_auto_choice_holds_under_sampled_reports():
+    """The kernels' report posts are sampled on steady traffic (ran on every 4th launch under variant
+    0, the mixed-length kernel's own mixed posts on every 32nd): 300 launches of mixed traffic keep
+    the mixed-length kernel from the first launch on, and 300 launches of uniform 1500-B traffic run
+    the 4-lane kernels and never the small-frame kernel (every sampled "ran" carries the long flag,
+    so no launch is counted short). Bit-exact at the end of each run."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    for label, (b, o, l), expect in (("mixed", synth.mixed_batch(4096, seed=31), {Engine.KERNEL_MIXED}),
+                                     ("uniform", synth.uniform_batch(4096, 1500, seed=32),
+                                      {Engine.KERNEL_MIXED, Engine.KERNEL_ONE_PASS})):
+        e = Engine(0)
+        try:
+            t = _dev_batch(b, o, l)
+            seen = []
+            for i in range(300):
+                out, st = e.digest_device(*t)
+                seen.append(e.last_kernel())
+                if i == 0 or i % 25 == 24:
+                    torch.cuda.synchronize()  # let reports land now and then, as a paced caller would
+            torch.cuda.synchronize()
+            assert set(seen) <= expect, (label, sorted(set(seen)))
+            if label == "uniform":
+                assert seen[-1] == Engine.KERNEL_ONE_PASS, seen[-5:]
+            _exact(out, st, b, o, l, f"sampled reports, {label}")
+        finally:
+            e.close()
+
+
 def test_variant8_leaves_small_kernel_on_jumbo_frames():
     """with variant 8 a batch of jumbo frames runs the small-frame kernel only
     until its long report arrives; the launches after it run the 4-lane kernels, within 2x of the
