@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import engines  # noqa: E402
 import framegen  # noqa: E402
 from oracle import coracle  # noqa: E402
-from seqs_amd import split_digests, synth  # noqa: E402
+from seqs_amd import FCS_APPEND, FILL_CSUM, split_digests, synth  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -27,8 +27,9 @@ torch = pytest.importorskip("torch")
 N_BATCHES = int(os.environ.get("FS_STRESS_BATCHES", "8"))
 
 
-def random_batch(seed: int):
-    """(buf, offsets, lengths, mtu): 1 to ~6,000 frames of one of four shapes."""
+def random_batch(seed: int, room: int = 0):
+    """(buf, offsets, lengths, mtu): 1 to ~6,000 frames of one of four shapes; `room` spare bytes at
+    least after every frame (a TX fill appends its FCS there)."""
     rnd = random.Random(seed)
     rng = np.random.default_rng(seed)
     kind = seed % 4
@@ -62,7 +63,7 @@ def random_batch(seed: int):
     for i, f in enumerate(frames):
         pos = (pos + align - 1) // align * align
         offsets[i] = pos
-        pos += len(f) + rnd.choice((0, 0, 0, 1, 4, 13, 64))
+        pos += len(f) + max(room, rnd.choice((0, 0, 0, 1, 4, 13, 64)))
     buf = np.zeros(pos + 64, np.uint8)
     for o, f in zip(offsets, frames):
         buf[int(o):int(o) + len(f)] = np.frombuffer(f, np.uint8)
@@ -95,5 +96,44 @@ def test_random_batches_every_variant(variant):
             hout, hst = e.digest_host(buf, off.astype(np.uint64), ln.astype(np.uint32), mtu=mtu)
             assert np.array_equal(hout["crc32"], dig["crc32"]) and np.array_equal(hout["ip_csum"], dig["ip_csum"])
             assert np.array_equal(hout["l4_csum"], dig["l4_csum"]) and np.array_equal(hst, est), f"seed {1000 + seed}, host"
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("variant", engines.VARIANTS, ids=engines.IDS)
+def test_random_fill_then_fcs_verify(variant):
+    """TX fill in place (fs_fill_batch, every flag combination) on the random batches, byte for byte
+    and digest for digest against the oracle's fill; then the FCS verify (fs_digest_batch_fcs) of
+    the wire frames it wrote, against the oracle's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    dev = torch.device("cuda:0")
+    e = engines.engine_for(variant)
+    try:
+        for seed in range(N_BATCHES):
+            buf, off, ln, mtu = random_batch(2000 + seed, room=4)
+            flags = (FILL_CSUM, FCS_APPEND, FILL_CSUM | FCS_APPEND, 0)[seed % 4]
+            tb = torch.from_numpy(buf.copy()).to(dev)
+            to, tl = torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)
+            out, st = e.fill_device(tb, to, tl, mtu=mtu, flags=flags)
+            torch.cuda.synchronize()
+            ebuf = buf.copy()
+            edig, est = coracle.fill_batch(ebuf, off, ln, mtu, flags)
+            gbuf = tb.cpu().numpy()
+            diff = np.nonzero(gbuf != ebuf)[0]
+            assert diff.size == 0, f"seed {2000 + seed} flags {flags}: {diff.size} bytes differ, first at {int(diff[0])}"
+            crc, ipc, l4c = split_digests(out.cpu().numpy())
+            stn = st.cpu().numpy()
+            bad = np.nonzero((crc != edig["crc32"]) | (ipc != edig["ip_csum"]) | (l4c != edig["l4_csum"]) | (stn != est))[0]
+            assert bad.size == 0, f"seed {2000 + seed} flags {flags}: {bad.size} fill digests differ, first {int(bad[0])}"
+            if flags & FCS_APPEND:
+                wl = (ln + 4).astype(np.int32)
+                fout, fst = e.digest_fcs_device(tb, to, torch.from_numpy(wl).to(dev), mtu=mtu)
+                torch.cuda.synchronize()
+                fdig, fest = coracle.digest_fcs_batch(ebuf, off, wl, mtu)
+                crc, ipc, l4c = split_digests(fout.cpu().numpy())
+                fstn = fst.cpu().numpy()
+                bad = np.nonzero((crc != fdig["crc32"]) | (ipc != fdig["ip_csum"]) | (l4c != fdig["l4_csum"]) | (fstn != fest))[0]
+                assert bad.size == 0, f"seed {2000 + seed}: {bad.size} FCS verifies differ, first {int(bad[0])}"
     finally:
         e.close()
