@@ -345,6 +345,77 @@ __global__ void __launch_bounds__(64 * WPB) k_span(const uint8_t* __restrict__ b
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// `c3seg`: the work-balanced segment pattern for mixed lengths, on the C3
+// layout (lengths cycling 64/576/1500/9000, packed back to back). A wave owns a tile of 16
+// consecutive frames; the frames' 64-B blocks (each frame's whole blocks, the block two frames
+// share counted for both) are concatenated and cut into 16 equal chunks, one per 4-lane group, so
+// every group streams the same number of block rows back to back through one ring, crossing frame
+// boundaries as it goes (no passes, no idle groups). Loads only: what the segment bookkeeping costs
+// per row is in the walk below (one compare per refill, a frame advance now and then).
+__device__ __forceinline__ uint64_t c3_start(uint32_t f) {
+    const uint32_t k = f & 3u;
+    return (uint64_t)(f >> 2) * 11140u + (k == 0u ? 0u : k == 1u ? 64u : k == 2u ? 640u : 2140u);
+}
+__device__ __forceinline__ uint32_t c3_len(uint32_t f) {
+    const uint32_t k = f & 3u;
+    return k == 0u ? 64u : k == 1u ? 576u : k == 2u ? 1500u : 9000u;
+}
+template <int PF, int WPB, int PASS = 0>
+__global__ void __launch_bounds__(64 * WPB) k_c3seg(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t* out) {
+    const uint32_t lane = threadIdx.x & 63u, grp = lane >> 2, gl = lane & 3u;
+    const uint32_t gwave = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    const uint32_t nwaves = gridDim.x * WPB;
+    const uint32_t ntiles = nframes / 16u;
+    uint32_t acc = 0;
+    for (uint32_t tile = gwave; tile < ntiles; tile += nwaves) {
+        const uint32_t f0 = tile * 16u;
+        // the tile's total blocks and this group's chunk [v0, v1) of the concatenation
+        uint32_t T = 0;
+        for (uint32_t j = 0; j < 16u; ++j) {
+            const uint64_t S = c3_start(f0 + j);
+            T += (uint32_t)((S + c3_len(f0 + j) - 1) / 64 - S / 64 + 1);
+        }
+        const uint32_t v0 = grp * T / 16u, v1 = (grp + 1u) * T / 16u;
+        const int R = (int)((T + 15u) / 16u);  // rows: the largest chunk
+        // the refill walk: frame j, its first block's virtual index vs and block count nb
+        uint32_t j = 0, vs = 0;
+        uint64_t b0 = c3_start(f0) / 64;
+        uint32_t nb = (uint32_t)((c3_start(f0) + c3_len(f0) - 1) / 64 - b0 + 1);
+        auto next_addr = [&](uint32_t v) -> const u32x4_a4* {
+            while (v >= vs + nb && j < 15u) {  // advance to the frame holding virtual block v
+                vs += nb;
+                ++j;
+                const uint64_t S = c3_start(f0 + j);
+                b0 = S / 64;
+                nb = (uint32_t)((S + c3_len(f0 + j) - 1) / 64 - b0 + 1);
+            }
+            return reinterpret_cast<const u32x4_a4*>(base + (b0 + (v - vs)) * 64u + 16u * gl);
+        };
+        // PASS > 0: the rows in passes of PASS rows with the ring drained at every pass end (the
+        // mixed-length kernel's pass structure: the next pass's first rows issued only after the
+        // pass's last block), to price the drains
+        constexpr int kPass = PASS > 0 ? PASS : 1 << 20;
+        for (int p0 = 0; p0 < R; p0 += kPass) {
+            const int pe = min(R, p0 + kPass);
+            u32x4 pf[PF];
+#pragma unroll
+            for (int i = 0; i < PF; ++i) {
+                const uint32_t v = v0 + (uint32_t)(p0 + i);
+                pf[i] = (p0 + i < pe && v < v1) ? *next_addr(v) : u32x4{0, 0, 0, 0};
+            }
+            for (int r0 = p0; r0 < pe; r0 += PF) {
+#pragma unroll
+                for (int i = 0; i < PF; ++i) {
+                    acc = (acc * 3u) ^ pf[i].x ^ pf[i].y ^ pf[i].z ^ pf[i].w;
+                    const uint32_t v = v0 + (uint32_t)(r0 + i + PF);
+                    if (r0 + i + PF < pe && v < v1) pf[i] = *next_addr(v);
+                }
+            }
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     // `dir [flen]`: forward-only (AL 2) against alternating-direction (AL 3) whole blocks
     const bool dir = argc > 1 && std::string(argv[1]).rfind("dir", 0) == 0;
@@ -448,6 +519,51 @@ int main(int argc, char** argv) {
             TILESM(16, 6, 0, 1);
             TILESM(16, 5, 0, 0);
             TILESM(16, 5, 0, 1);
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "c3seg") {
+        // the C3 layout (65,536 frames, 182.5 MB) in the first NB buffers' place: plain stream over
+        // the same bytes against the segment pattern
+        const uint32_t n3 = 65536;
+        const size_t b3 = (size_t)n3 / 4 * 11140;
+        std::vector<uint8_t*> c3(4);
+        for (auto& b : c3) {
+            CHECK(hipMalloc(&b, b3 + 4096));
+            CHECK(hipMemset(b, 0x5a, b3 + 4096));
+        }
+        auto run3 = [&](auto launch, const char* name) {
+            double res[2];
+            int k = 0;
+            for (int ns : {1, 4}) {
+                for (int pass = 0; pass < 2; ++pass) {
+                    CHECK(hipDeviceSynchronize());
+                    auto t0 = std::chrono::steady_clock::now();
+                    for (int i = 0; i < reps; ++i) launch(i, st[i % ns]);
+                    CHECK(hipDeviceSynchronize());
+                    res[k] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+                }
+                ++k;
+            }
+            printf("C3 %-41s 1 stream %9.2f us %7.0f GB/s | 4 streams %9.2f us %7.0f GB/s\n", name, res[0],
+                   b3 / (res[0] * 1e-6) / 1e9, res[1], b3 / (res[1] * 1e-6) / 1e9);
+        };
+        for (int rep = 0; rep < 2; ++rep) {
+            run3([&](int i, hipStream_t s) {
+                hipLaunchKernelGGL((k_stream<4, 16>), dim3(cus), dim3(1024), 0, s, (const u32x4*)c3[i % 4], b3 / 16, out);
+            }, "stream PF=4 waves/WG=16");
+            run3([&](int i, hipStream_t s) {
+                hipLaunchKernelGGL((k_c3seg<5, 16>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, out);
+            }, "segments PF=5 waves/WG=16");
+            run3([&](int i, hipStream_t s) {
+                hipLaunchKernelGGL((k_c3seg<6, 16>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, out);
+            }, "segments PF=6 waves/WG=16");
+            run3([&](int i, hipStream_t s) {
+                hipLaunchKernelGGL((k_c3seg<6, 16, 12>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, out);
+            }, "segments PF=6, drained every 12 rows");
+            run3([&](int i, hipStream_t s) {
+                hipLaunchKernelGGL((k_c3seg<6, 16, 24>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, out);
+            }, "segments PF=6, drained every 24 rows");
         }
         return 0;
     }
