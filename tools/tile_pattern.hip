@@ -416,6 +416,127 @@ __global__ void __launch_bounds__(64 * WPB) k_c3seg(const uint8_t* __restrict__ 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// `c3segc`: the segment pattern above with the kernel's compute skeleton, to price a segment kernel
+// before building it. Per row each lane folds its 16 B into 4 dword streams with the
+// one-pass kernel's Z64 step (4 lookups in a conflict-free replicated 64-KB table, v_bitop3) and its
+// 4 v_sad_u16; when the row's block ends a segment (the frame's last block, or the chunk's), the
+// group parks its 16 streams and sum in LDS and restarts from zero (a divergent store: the wave runs
+// it whenever any group ends a segment on that row). After the rows each group combines its parked
+// segments (Z12/Z8/Z4 per lane, a lane shift, DPP), and one lane per frame folds its segments with
+// shifts and writes 8 B. Random table contents: results are not CRCs (loads, lookups and the
+// bookkeeping are the kernel's).
+constexpr int kSegMax = 4;  // parked segments per group (a C3 chunk of ~44 blocks spans up to 5: the 5th reuses the 4th slot here)
+template <int PF>
+__global__ void __launch_bounds__(1024) k_c3segc(const uint8_t* __restrict__ base, uint32_t nframes,
+                                                 uint2* __restrict__ dig, uint32_t* out) {
+    __shared__ __attribute__((aligned(16))) char lds[65536 + 16 * 16 * kSegMax * 80];
+    const uint32_t lane = threadIdx.x & 63u, grp = lane >> 2, gl = lane & 3u, wave = threadIdx.x >> 6;
+    for (uint32_t o = threadIdx.x * 16u; o < 65536u; o += 1024u * 16u)
+        *reinterpret_cast<u32x4*>(lds + o) = u32x4{o * 0x9E3779B1u, o ^ 0x5bd1e995u, o * 7u, ~o};
+    __syncthreads();
+    uint32_t cvec = 0, sel[4];
+    {
+        const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; ++jj) cvec |= (32u * jj + 4u * c) << (8u * jj);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t b = (k + h) & 3u;
+            sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
+        }
+    }
+    char* park = lds + 65536 + wave * (16 * kSegMax * 80);  // [group][seg]: 4 lanes x 16 B streams + sums
+    const uint32_t gwave = wave * gridDim.x + blockIdx.x;
+    const uint32_t nwaves = gridDim.x * 16u;
+    const uint32_t ntiles = nframes / 16u;
+    uint32_t acc = 0;
+    for (uint32_t tile = gwave; tile < ntiles; tile += nwaves) {
+        const uint32_t f0 = tile * 16u;
+        uint32_t T = 0;
+        for (uint32_t j = 0; j < 16u; ++j) {
+            const uint64_t S = c3_start(f0 + j);
+            T += (uint32_t)((S + c3_len(f0 + j) - 1) / 64 - S / 64 + 1);
+        }
+        const uint32_t v0 = grp * T / 16u, v1 = (grp + 1u) * T / 16u;
+        const int R = (int)((T + 15u) / 16u);
+        uint32_t j = 0, vs = 0;
+        uint64_t b0 = c3_start(f0) / 64;
+        uint32_t nb = (uint32_t)((c3_start(f0) + c3_len(f0) - 1) / 64 - b0 + 1);
+        // the refill walk; `last` = the block ends a segment (its frame's last, or the chunk's)
+        auto next_addr = [&](uint32_t v, bool& last) -> const u32x4_a4* {
+            while (v >= vs + nb && j < 15u) {
+                vs += nb;
+                ++j;
+                const uint64_t S = c3_start(f0 + j);
+                b0 = S / 64;
+                nb = (uint32_t)((S + c3_len(f0 + j) - 1) / 64 - b0 + 1);
+            }
+            last = v + 1u == vs + nb || v + 1u == v1;
+            return reinterpret_cast<const u32x4_a4*>(base + (b0 + (v - vs)) * 64u + 16u * gl);
+        };
+        u32x4 pf[PF];
+        uint32_t lastbits = 0;  // ring slot i ends a segment: bit i
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const uint32_t v = v0 + (uint32_t)i;
+            bool l = false;
+            pf[i] = (i < R && v < v1) ? *next_addr(v, l) : u32x4{0, 0, 0, 0};
+            lastbits |= (l ? 1u : 0u) << i;
+        }
+        uint32_t A0 = 0, A1 = 0, A2 = 0, A3 = 0, cs = 0, nseg = 0;
+        for (int r0 = 0; r0 < R; r0 += PF) {
+#pragma unroll
+            for (int i = 0; i < PF; ++i) {
+                const u32x4 w = pf[i];
+                A0 = span_z<0>(lds, A0, cvec, sel, w.x);
+                A1 = span_z<0>(lds, A1, cvec, sel, w.y);
+                A2 = span_z<0>(lds, A2, cvec, sel, w.z);
+                A3 = span_z<0>(lds, A3, cvec, sel, w.w);
+                cs = __builtin_amdgcn_sad_u16(w.x, 0u, cs);
+                cs = __builtin_amdgcn_sad_u16(w.y, 0u, cs);
+                cs = __builtin_amdgcn_sad_u16(w.z, 0u, cs);
+                cs = __builtin_amdgcn_sad_u16(w.w, 0u, cs);
+                if ((lastbits >> i) & 1u) {  // park the finished segment, restart the streams
+                    const uint32_t slot = (grp * kSegMax + min(nseg, (uint32_t)kSegMax - 1u)) * 80u;
+                    *reinterpret_cast<u32x4*>(park + slot + 16u * gl) = u32x4{A0, A1, A2, A3};
+                    *reinterpret_cast<uint32_t*>(park + slot + 64u + 4u * gl) = cs;
+                    A0 = A1 = A2 = A3 = cs = 0u;
+                    ++nseg;
+                }
+                const uint32_t v = v0 + (uint32_t)(r0 + i + PF);
+                bool l = false;
+                if (r0 + i + PF < R && v < v1) pf[i] = *next_addr(v, l);
+                lastbits = (lastbits & ~(1u << i)) | ((l ? 1u : 0u) << i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // combine each group's parked segments: per lane Z12/Z8/Z4 + its lane shift, DPP over the group
+        const uint32_t ns = min(nseg, (uint32_t)kSegMax);
+        for (uint32_t k = 0; k < ns; ++k) {
+            const uint32_t slot = (grp * kSegMax + k) * 80u;
+            const u32x4 a = *reinterpret_cast<const u32x4*>(park + slot + 16u * gl);
+            uint32_t u = span_z<0>(lds, a.x, cvec, sel, 0u) ^ span_z<0>(lds, a.y, cvec, sel, 0u) ^
+                         span_z<0>(lds, a.z, cvec, sel, 0u) ^ a.w;
+            u = span_z<0>(lds, u, cvec, sel, 0u);
+            u ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0xB1, 0xf, 0xf, false);
+            u ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)u, 0x4E, 0xf, 0xf, false);
+            uint32_t c = *reinterpret_cast<const uint32_t*>(park + slot + 64u + 4u * gl);
+            c += (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0xB1, 0xf, 0xf, false);
+            c += (uint32_t)__builtin_amdgcn_mov_dpp((int)c, 0x4E, 0xf, 0xf, false);
+            if (gl == 0u) *reinterpret_cast<uint2*>(park + slot) = make_uint2(u, c);
+        }
+        // one lane per frame: fold two segments' values with a shift (a frame spans 1 to 4 chunks)
+        if (lane < 16u) {
+            const uint2 y0 = *reinterpret_cast<const uint2*>(park + (lane * kSegMax) * 80u);
+            const uint2 y1 = *reinterpret_cast<const uint2*>(park + ((lane ^ 1u) * kSegMax + 1u) * 80u);
+            uint32_t y = span_z<0>(lds, span_z<0>(lds, y0.x, cvec, sel, 0u), cvec, sel, y1.x);
+            y = span_z<0>(lds, y, cvec, sel, 0u);
+            dig[f0 + lane] = make_uint2(y, y0.y + y1.y);
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     // `dir [flen]`: forward-only (AL 2) against alternating-direction (AL 3) whole blocks
     const bool dir = argc > 1 && std::string(argv[1]).rfind("dir", 0) == 0;
@@ -532,6 +653,8 @@ int main(int argc, char** argv) {
             CHECK(hipMalloc(&b, b3 + 4096));
             CHECK(hipMemset(b, 0x5a, b3 + 4096));
         }
+        uint2* dig3;
+        CHECK(hipMalloc(&dig3, (size_t)n3 * sizeof(uint2)));
         auto run3 = [&](auto launch, const char* name) {
             double res[2];
             int k = 0;
@@ -558,6 +681,12 @@ int main(int argc, char** argv) {
             run3([&](int i, hipStream_t s) {
                 hipLaunchKernelGGL((k_c3seg<6, 16>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, out);
             }, "segments PF=6 waves/WG=16");
+            run3([&](int i, hipStream_t s) {
+                hipLaunchKernelGGL((k_c3segc<5>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, dig3, out);
+            }, "segments + compute skeleton PF=5");
+            run3([&](int i, hipStream_t s) {
+                hipLaunchKernelGGL((k_c3segc<6>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, dig3, out);
+            }, "segments + compute skeleton PF=6");
             run3([&](int i, hipStream_t s) {
                 hipLaunchKernelGGL((k_c3seg<6, 16, 12>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, out);
             }, "segments PF=6, drained every 12 rows");
