@@ -151,9 +151,11 @@ fs_status fs_digest_batch_fcs(fs_ctx* ctx, const uint8_t* frames, const uint64_t
  * RecvEth): stages H2D, runs the kernel and copies D2H on the context's
  * stream, returning when the results are in `out`/`status`. Pinned memory
  * (fs_host_alloc) gives full PCIe rate; pageable memory works (offsets, lengths, out and status
- * that are pinned are copied straight from / to, the others through the context's pinned mirror).
- * With fs_ctx_set_kernel 0 or 8 a batch whose frames are all <= 128 bytes runs the small-frame
- * kernel: the lengths are on the host here. */
+ * that are pinned are copied straight from / to, or written by the kernel in place, the others go
+ * through the context's pinned mirror; an array counts as pinned only when all of it lies inside
+ * one pinned allocation). With fs_ctx_set_kernel 0 or 8 a batch whose frames are all <= 128 bytes
+ * runs the small-frame kernel: the lengths are on the host here; when its frames, offsets and
+ * lengths are all pinned, that kernel reads them in place over PCIe (one launch, no copy). */
 fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                                const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status);
 
