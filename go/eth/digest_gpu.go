@@ -124,7 +124,8 @@ func (g *GPU) SetKernel(variant int) error {
 // reads the 64-byte blocks around each frame inside its own staging buffer). The frames'
 // offsets and lengths go into the same pinned allocation, after the frames, so that
 // fs_digest_batch_host copies them to the device straight from there (no mirror copy on the
-// host; DESIGN.md §5.3). The device reads the pinned buffer over PCIe.
+// host; DESIGN.md §5.3), and a batch of short frames (all <= 128 B, the reference's benchmark
+// shape) is read in place over PCIe by the small-frame kernel: one launch, no copy.
 func (g *GPU) stage(frames [][]byte, spare int) ([]byte, error) {
 	n := len(frames)
 	total := 0
