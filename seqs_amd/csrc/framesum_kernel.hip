@@ -1883,9 +1883,10 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
     if (force == 2 || force == 4) mixed = force == 2;
     // The small-frame kernel (RX digest and FCS verify; a TX fill keeps the 4-lane choice above).
-    // The kernels report every launch that met a frame longer than kSmallMaxLen (kReportLong), and
-    // the 4-lane kernels every launch that ran (kReportRan, posted after its first workgroup's own
-    // long flag); the host counts the launches it sees run since the latest long report. Variant 0
+    // The kernels report launches that met a frame longer than kSmallMaxLen (kReportLong), and the
+    // 4-lane kernels, when asked (kAskRan), that a launch ran (kReportRan, with the grid's first
+    // tile's own long flag in the same word, kReportRanLong); the host counts the launches it sees
+    // run since the latest long report. Variant 0
     // moves to the small-frame kernel after kShortLaunchesAuto of them; variant 8 runs it until a
     // long report arrives, then the 4-lane choice until kShortLaunchesSmall launches ran short
     // again. The reports come launches late, so a long frame can still meet the small-frame kernel:
