@@ -90,8 +90,9 @@ typedef struct fs_ctx fs_ctx;
 uint32_t fs_abi_version(void);
 int fs_device_count(void);
 
-/* Context: owns the device copy of the CRC shift tables, staging buffers and
- * an internal stream for the host-staged entry point. */
+/* Context: owns the device copy of the CRC shift tables, a host-mapped report block (the
+ * automatic kernel choice), the host-staged entry points' staging buffers and pinned mirrors,
+ * and three internal streams for them (a compute stream and two copy streams). */
 fs_status fs_ctx_create(int device, fs_ctx** out);
 fs_status fs_ctx_destroy(fs_ctx* ctx);
 /* Message for the last failing call on `ctx` (or of fs_ctx_create when ctx is NULL). */

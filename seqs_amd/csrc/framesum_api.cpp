@@ -246,7 +246,9 @@ hipError_t launch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, c
 constexpr uint32_t kSmallAutoMaxLen = framesum::kSmallMaxLen;
 int host_force(const fs_ctx* ctx, uint32_t max_len) {
     if (ctx->force_kernel != 0 && ctx->force_kernel != 8) return ctx->force_kernel;
-    return max_len <= kSmallAutoMaxLen ? framesum::kForceSmallExact : 0;
+    // a longer frame: the 4-lane choice, never the small-frame kernel, even after a
+    // streak of short device-resident launches
+    return max_len <= kSmallAutoMaxLen ? framesum::kForceSmallExact : framesum::kForceNoSmall;
 }
 
 }  // namespace
@@ -411,10 +413,6 @@ FS_HOST_CLONES static framesum::plan::ScanCore scan_descriptors(const uint64_t* 
     return framesum::plan::scan_core(offsets, lengths, n);
 }
 
-// A host-staged batch that fits one staging chunk (every batch of short frames): one H2D copy of
-// the frames and one of the descriptors on the two copy streams at once, one launch, the results'
-// D2H, and a polled wait. Descriptors and results go straight from / to the caller's arrays when
-// those are pinned (fs_host_alloc), through the context's pinned mirror otherwise.
 // The device address of pinned host memory [p, p + bytes) the kernel can read or write directly, or
 // null.
 static void* mapped(void* p, size_t bytes) {
@@ -427,6 +425,11 @@ static void* mapped(void* p, size_t bytes) {
     return d;
 }
 
+// A host-staged batch that fits one staging chunk (path 1). Everything runs on the compute stream,
+// in its order: the descriptor copy (queued by the caller before its scan, straight from the
+// caller's arrays when they are pinned), the frames' H2D copy into slot 0, one launch that writes the
+// digests and verdicts into host memory through a mapped pointer (the caller's arrays when pinned,
+// else the context's mirror, copied out after the wait; no D2H copy), then a polled wait.
 static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames_bytes, const uint64_t* offsets,
                              const uint32_t* lengths, uint32_t n, uint32_t mtu, fs_digest* out, uint8_t* status,
                              const framesum::plan::Scan& sc, int force) {
@@ -435,7 +438,11 @@ static fs_status host_single(fs_ctx* ctx, const uint8_t* frames, uint64_t frames
     framesum::plan::copy_span(sc.lo, sc.hi, frames_bytes, cpy_lo, cpy_hi);
     HostSlot& sl = ctx->slot[0];
     fs_status st = ensure_slot(ctx, sl, cpy_hi - cpy_lo + 64, n);
-    if (st != FS_SUCCESS) return st;
+    if (st != FS_SUCCESS) {
+        // the descriptor copy already queued may still read the caller's arrays
+        drain_host_streams(ctx);
+        return st;
+    }
     // The kernel writes the digests and verdicts straight to host memory (mapped pinned memory: no
     // D2H copy, no gap before it): into the caller's arrays when they are pinned, else into the
     // context's pinned mirror, copied out after the wait.
@@ -869,7 +876,12 @@ int fs_test_last_host_path(const fs_ctx* ctx) { return ctx ? ctx->last_host_path
 fs_status fs_host_alloc(fs_ctx* ctx, uint64_t bytes, void** out) {
     if (!ctx || !out) return FS_E_INVALID;
     *out = nullptr;
-    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess)
+    // Mapped (the in-place read and the direct result writes take its device address) and portable
+    // (fs_digest_batch_multi's other contexts address it too). Coarse-grained: a kernel may cache its
+    // lines in L2, but every launch begins with a system-scope acquire (HIP's dispatch packets), which
+    // invalidates them, so a buffer the caller refills between calls is read anew
+    // (test_host_inplace_refilled_buffer runs 200 refills of one buffer through the in-place path).
+    if (hipHostMalloc(out, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
         return set_err(ctx, FS_E_NOMEM, "hipHostMalloc failed");
     return FS_SUCCESS;
 }

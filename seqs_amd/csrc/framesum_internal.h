@@ -83,9 +83,12 @@ constexpr uint32_t kRanSample = 4, kMixedSample = 32;
 // launches seen to run without a long frame before variant 0 moves to the small-frame kernel, and
 // before a variant-8 context that met long frames goes back to it
 constexpr uint32_t kShortLaunchesAuto = 16, kShortLaunchesSmall = 2;
-// launch_digest's force value for the host-staged path, which knows every length: the small-frame
-// kernel unconditionally
+// launch_digest's force values for the host-staged path, which knows every length: the small-frame
+// kernel unconditionally (every frame <= kSmallMaxLen), or the automatic choice among the 4-lane
+// kernels only (a frame is longer: however short the context's recent traffic, the small-frame
+// kernel would stream that frame with one lane)
 constexpr int kForceSmallExact = 16;
+constexpr int kForceNoSmall = 17;
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
                          int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, uint32_t* next_id,

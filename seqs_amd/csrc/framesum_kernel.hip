@@ -1893,6 +1893,9 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     // it stays correct there, only slower (one lane streams it). kForceSmallExact: the host-staged
     // path, which has seen every length.
     bool small = false;
+    // kForceNoSmall (a host-staged batch with a long frame) reports as the automatic choice does, so
+    // its long frames end a short streak; it only never picks the small-frame kernel itself
+    const bool autov = force == 0 || force == kForceNoSmall;
     if (can_report) {
         const uint32_t lng = report_host[kReportLong], rw = report_host[kReportRan], ran = rw & 0xFFFFu;
         const bool ran_new = ran != report_host[kReportRanSeen];
@@ -1908,16 +1911,16 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         if (force == 0) small = streak >= kShortLaunchesAuto;
         if (force == 8) small = report_host[kReportLongEver] == 0u || streak >= kShortLaunchesSmall;
         // every workgroup reports its long frames while the host counts short launches
-        if ((force == 0 || force == 8) && streak > 0u) report |= 1ull << 47;
+        if ((autov || force == 8) && streak > 0u) report |= 1ull << 47;
         // "ran": variant 0 samples it on long traffic and asks every launch while it counts short
         // ones; variant 8 (short traffic expected: back to the small-frame kernel after 2 short
         // launches) asks every launch
-        if (force == 8 || (force == 0 && (streak > 0u || seq % kRanSample == 0u))) report |= kAskRan;
+        if (force == 8 || (autov && (streak > 0u || seq % kRanSample == 0u))) report |= kAskRan;
     } else if (force == 8) {
         small = true;  // no report block: the caller's choice as it stands
     }
     if (force == kForceSmallExact) small = true;
-    if (op == FsOp::kFill) small = false;
+    if (force == kForceNoSmall || op == FsOp::kFill) small = false;
     if (small) mixed = false;
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {

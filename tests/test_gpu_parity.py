@@ -707,3 +707,53 @@ def test_host_small_batch_read_in_place(pinned_results):
                 assert np.array_equal(out["l4_csum"], dig["l4_csum"]) and np.array_equal(st, est)
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("pinned_results", [False, True])
+def test_host_inplace_refilled_buffer(pinned_results):
+    """ONE fs_host_alloc frames buffer and ONE descriptor buffer, refilled by the host
+    with new random contents before each of 200 in-place calls (path 2, as the Go binding reuses its
+    staging buffer): every call reads the new bytes, never lines cached from an earlier launch.
+    Lengths, offsets and contents change per call; pinned and pageable result arrays."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from seqs_amd.framesum import DIGEST_DTYPE, TEST_LIB_PATH
+
+    e = Engine(0, lib_path=TEST_LIB_PATH)
+    try:
+        n, cap = 2048, 2048 * 132 + 64
+        pin = e.host_empty((cap,), np.uint8)
+        desc = e.host_empty((12 * n,), np.uint8)
+        poff, plen = desc[: 8 * n].view(np.uint64), desc[8 * n:].view(np.uint32)
+        if pinned_results:
+            out, st = e.host_empty((n,), DIGEST_DTYPE), e.host_empty((n,), np.uint8)
+        else:
+            out, st = np.zeros(n, DIGEST_DTYPE), np.zeros(n, np.uint8)
+        for it in range(200):
+            rng = np.random.default_rng(1000 + it)
+            hb, ho, hl = synth.hello_batch(n, seed=it)
+            ln = rng.integers(0, 129, size=n).astype(np.uint32)
+            valid = rng.random(n) < 0.5  # half the frames: valid UDP frames (47 B), checksums verified
+            ln[valid] = hl[valid]
+            gaps = rng.integers(0, 4, size=n).astype(np.uint64)
+            off = np.zeros(n, np.uint64)
+            off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + gaps[:-1])
+            off += np.uint64(rng.integers(0, 4))
+            assert int(off[-1]) + int(ln[-1]) <= cap
+            buf = rng.integers(0, 256, size=cap, dtype=np.uint8)
+            for i in np.nonzero(valid)[0]:
+                o = int(off[i])
+                buf[o:o + int(ln[i])] = hb[int(ho[i]):int(ho[i]) + int(hl[i])]
+            pin[:] = buf
+            poff[:] = off
+            plen[:] = ln
+            out[:] = np.zeros(1, DIGEST_DTYPE)
+            st[:] = 0xFF
+            e.digest_host(pin, poff, plen, out=out, status=st)
+            assert e.lib.fs_test_last_host_path(e._ctx) == 2
+            dig, est = coracle.digest_batch(buf, off.astype(np.int64), ln.astype(np.int32), nthreads=8)
+            bad = np.nonzero((out["crc32"] != dig["crc32"]) | (out["ip_csum"] != dig["ip_csum"]) |
+                             (out["l4_csum"] != dig["l4_csum"]) | (st != est))[0]
+            assert bad.size == 0, (it, bad[:5])
+    finally:
+        e.close()
