@@ -520,7 +520,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
     FS_HIP(ctx, hipSetDevice(ctx->device));
     fs_status pst = quiesce_host_streams(ctx);
     if (pst != FS_SUCCESS) return pst;
-    if (n <= kChunkFrames && ctx->force_kernel != 2 && ctx->force_kernel != 4) {
+    if (n <= kChunkFrames && ctx->force_kernel != 2 && ctx->force_kernel != 3 && ctx->force_kernel != 4) {
         // A batch of short frames whose frames, offsets and lengths are all in pinned host memory:
         // the small-frame kernel reads them in place over PCIe and writes its results to host
         // memory, so the call is one launch -- no copies, no gaps between DMA commands.
@@ -842,8 +842,8 @@ fs_status fs_ctx_set_workgroups(fs_ctx* ctx, int workgroups) {
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant) {
     if (!ctx) return FS_E_INVALID;
     ctx->err.clear();
-    if (variant != 0 && variant != 2 && variant != 4 && variant != 8)
-        return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0 (automatic), 2, 4 or 8");
+    if (variant != 0 && variant != 2 && variant != 3 && variant != 4 && variant != 8)
+        return set_err(ctx, FS_E_INVALID, "fs_ctx_set_kernel: variant must be 0 (automatic), 2, 3, 4 or 8");
     ctx->force_kernel = variant;
     return FS_SUCCESS;
 }

@@ -32,7 +32,12 @@ struct FsTables {
     // T[b][1 << j] of the 40 plain [4][256] tables above, in LDS-image order (piece p = 4 t + b is the
     // 1-KB piece at LDS byte 1024 p): the kernels build them in place by VALU, as region A
     uint32_t plain_basis[40][8];
+    // The segment kernel's binary shift tables Z_128, Z_256, ..., Z_2048 ([4][256] each, 20 1-KB pieces
+    // after its scratch in LDS; built in place from these bases like the plain tables): a segment's
+    // value is shifted to its frame's end in at most ~10 lookup rounds
+    uint32_t zbin_basis[20][8];
 };
+constexpr int kZbinTables = 5;  // Z_(128 << i), i = 0..4
 constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 10;  // the LDS image: everything before z64_basis
 static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout");
 static_assert(offsetof(FsTables, z32) == 65536 && offsetof(FsTables, plain_basis) == kTablesLdsBytes + 128,

@@ -1117,6 +1117,36 @@ struct LayA1 : LayoutA {
     }
 };
 
+// The 16 streams of a group combined to the frame's last dword, at block position q = 15 - ealign
+// of the last row (the block-aligned combine). Stream j of lane gl (row position
+// 4 gl + j) is shifted by its distance in dwords to q: s = (K - j) mod 16 with K = (q - 4 gl) mod 16
+// = 4 a + C (the streams past q skipped the last row). Streams j <= C need Z_(16 a) Z_(4 (C - j)),
+// the others Z_(16 ((a - 1) & 3)) Z_(4 (4 + C - j)). Sorted by their Z4 class c (B_c = A_((C - c) & 3):
+// the registers reversed, then rotated by C), that is one round of Z4 / Z8 / Z12 with a fixed table
+// per register and one round of Z_(16 a) per class: 5 lookups in 2 dependent rounds, then the XOR
+// over the group's 4 lanes by DPP (tests/kernel_model.py).
+template <class Lay>
+__device__ __forceinline__ uint32_t combine_to_end(const char* lds, const uint32_t (&A)[4], int ealign, uint32_t gl) {
+    const uint32_t K = (uint32_t)(15 - ealign - 4 * (int)gl) & 15u;
+    const uint32_t a = K >> 2, C = K & 3u;
+    uint32_t Y;
+    {
+        const bool r1 = (C & 1u) != 0u, r2 = (C & 2u) != 0u;
+        // reversed: (A0, A3, A2, A1); rotated by 1 then by 2 where C has those bits
+        const uint32_t x0 = r1 ? A[1] : A[0], x1 = r1 ? A[0] : A[3], x2 = r1 ? A[3] : A[2], x3 = r1 ? A[2] : A[1];
+        const uint32_t b0 = r2 ? x2 : x0, b1 = r2 ? x3 : x1, b2 = r2 ? x0 : x2, b3 = r2 ? x1 : x3;
+        const uint32_t t1 = zplain(lds, b1, kLdsZfin);  // Z4
+        const uint32_t t2 = zplain(lds, b2, kLdsZ8);
+        const uint32_t t3 = zplain(lds, b3, kLdsZ12);
+        const uint32_t v1 = b0 ^ (C >= 1u ? t1 : 0u) ^ (C >= 2u ? t2 : 0u) ^ (C == 3u ? t3 : 0u);
+        const uint32_t v2 = xor3(b0 ^ t1, t2, t3) ^ v1;
+        Y = Lay::z16a(lds, v1, a) ^ Lay::z16a(lds, v2, (a - 1u) & 3u);
+    }
+    Y ^= dpp_quad<kQuadXor1>(Y);
+    Y ^= dpp_quad<kQuadXor2>(Y);
+    return Y;
+}
+
 // `report` = the host-mapped report block's address in bits 0..46, the watch flag in bit 47, the launch
 // id in bits 48..63
 // (one kernel argument, loaded where it is used: nothing of it stays live through the tile loop).
@@ -1375,33 +1405,10 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         }
         FS_STAMP(2);
 
-        // ---- combine the 16 streams of each frame. Stream j of lane gl (row position 4 gl + j)
-        // is shifted by its distance in dwords to the frame's last dword, at position
-        // q = 15 - ealign() of the last row: s = (K - j) mod 16 with K = (q - 4 gl) mod 16 = 4 a + C
-        // (the streams past q skipped the last row); then xor over the group's 4 lanes.
-        // Streams j <= C need Z_(16 a) Z_(4 (C - j)), the others Z_(16 ((a - 1) & 3)) Z_(4 (4 + C - j)).
-        // Sorted by their Z4 class c (B_c = A_((C - c) & 3): the registers reversed, then rotated
-        // by C), that is one round of Z4 / Z8 / Z12 with a fixed table per register and one round
-        // of Z_(16 a) per class: 5 lookups in 2 dependent rounds (tests/kernel_model.py).
+        // ---- combine the 16 streams of each frame to its last dword (combine_to_end).
         // The parked parse, read by every lane now: its LDS round trip overlaps the combine's.
         const Parsed P = unpark_parsed<kOps>(lds, hw, grp);
-        const uint32_t K = (uint32_t)(15 - T.ealign() - 4 * (int)gl) & 15u;
-        const uint32_t a = K >> 2, C = K & 3u;
-        uint32_t Y;
-        {
-            const bool r1 = (C & 1u) != 0u, r2 = (C & 2u) != 0u;
-            // reversed: (A0, A3, A2, A1); rotated by 1 then by 2 where C has those bits
-            const uint32_t x0 = r1 ? A[1] : A[0], x1 = r1 ? A[0] : A[3], x2 = r1 ? A[3] : A[2], x3 = r1 ? A[2] : A[1];
-            const uint32_t b0 = r2 ? x2 : x0, b1 = r2 ? x3 : x1, b2 = r2 ? x0 : x2, b3 = r2 ? x1 : x3;
-            const uint32_t t1 = zplain(lds, b1, kLdsZfin);  // Z4
-            const uint32_t t2 = zplain(lds, b2, kLdsZ8);
-            const uint32_t t3 = zplain(lds, b3, kLdsZ12);
-            const uint32_t v1 = b0 ^ (C >= 1u ? t1 : 0u) ^ (C >= 2u ? t2 : 0u) ^ (C == 3u ? t3 : 0u);
-            const uint32_t v2 = xor3(b0 ^ t1, t2, t3) ^ v1;
-            Y = Lay::z16a(lds, v1, a) ^ Lay::z16a(lds, v2, (a - 1u) & 3u);
-        }
-        Y ^= dpp_quad<kQuadXor1>(Y);
-        Y ^= dpp_quad<kQuadXor2>(Y);
+        const uint32_t Y = combine_to_end<Lay>(lds, A, T.ealign(), gl);
         // checksum over the 4 lanes of the group, each lane first folded mod 65535 (the finish
         // only needs the total mod 65535; the fold keeps every partial < 2^18)
         cs = (cs & 0xffffu) + (cs >> 16);
@@ -1656,6 +1663,485 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 
 
 // =======================================================================================
+// The SEGMENT kernel (digest_kernel_g, variant 2 since round 6): mixed lengths on
+// the one-pass kernel's block-aligned rows, with no idle group and no pass. A tile's frames, as the
+// 64-B blocks that hold them, are concatenated in frame order (a frame with no stream dword takes no
+// block; the others are numbered by RANK) into T virtual blocks, cut into 16 CHUNKS of
+// L = ceil(T / 16) blocks, one per 4-lane group: every group streams L rows back to back through one
+// ring, crossing frame boundaries. A SEGMENT is the part of one frame inside one chunk. The row that
+// ends a segment (the frame's last block, or the chunk's last) PARKS the group's 16 streams in LDS
+// and restarts them from zero, so the row loop never combines; a frame's head rows (its first block,
+// and its second when frame dword 1 lies there) mask the bytes before the frame and apply the CRC
+// init; its last block masks the bytes past its end and leaves the streams past its last dword as
+// they were (the one-pass tail row). Those rows are EVENTS of the lanes they concern: a divergent
+// branch before and after the row's lean update, which the wave runs when any of its lanes has an
+// event (about 30 rows of a C3 tile's 45). A tile has at most 16 + 15 = 31 segments, and segment
+// (rank k, group g) parks in slot k + g: no per-tile bound, no fallback. After the rows group
+// s mod 16 combines slot s as the one-pass kernel combines a frame (to the frame's last dword for
+// the segment that ends the frame, to the block end for one cut by its chunk) and shifts it by its
+// distance to the frame end; a frame's register is the XOR of its segments' values and its sum the
+// sum of theirs (tests/kernel_model.py: crc32_tile_segments).
+constexpr int kRingG = 5;
+constexpr int kSlotG = 16;  // header slot dwords (1 KB per wave; longer headers come from memory)
+constexpr uint32_t kHdrWaveG = 4u * kSlotG * kFramesPerTile;
+constexpr uint32_t kLdsHdrG = kLdsTables;
+constexpr uint32_t kLdsWaveG = kLdsHdrG + kWavesPerBlock * kHdrWaveG;
+// Per-wave scratch: the frame table by rank (16 B: {delta lo, delta hi, vend, info}; block v of the
+// tile lies at delta + 64 v), the rank-indexed vend table (~0 past the last rank: the walks' starting
+// search), the parked checksums (one per slot, folded over the group; a combined slot's {value, sum}
+// after the combine), the slot meta (the rank of the frame parked there; ~0 = unused), and each
+// group's frame (read back by the parse and the finish: no register holds it through the rows).
+constexpr uint32_t kGFtab = 0, kGVend = 256, kGPcs = 320, kGMeta = 576, kGFrame = 704;
+constexpr uint32_t kGScratch = 960;
+constexpr uint32_t kSegSlots = 2u * kFramesPerTile - 1u;
+static_assert(kLdsWaveG + kWavesPerBlock * kGScratch <= kLdsBytes, "segment kernel LDS");
+static_assert(kGPcs - kGVend >= 4u * kFramesPerTile && kGMeta - kGPcs >= 8u * (kSegSlots + 1u) &&
+                  kGFrame - kGMeta >= 4u * (kSegSlots + 1u) && kGScratch - kGFrame >= 16u * kFramesPerTile,
+              "segment scratch");
+// Parked streams: region A's upper halves (bytes 128..255 of its 256-B entries, which no lookup
+// reads): wave w owns entries 16 w .. 16 w + 15, two 64-B slots each.
+__device__ __forceinline__ uint32_t park_at(uint32_t wave, uint32_t s) {
+    return kLdsRegionA + (16u * wave + (s >> 1)) * 256u + 128u + 64u * (s & 1u);
+}
+// The binary shift tables Z_128 .. Z_2048 after the scratch (FsTables::zbin_basis), built in place
+constexpr uint32_t kLdsZbinG = kLdsWaveG + kWavesPerBlock * kGScratch;
+static_assert(kLdsZbinG + 4096u * kZbinTables <= kLdsBytes, "segment kernel shift tables");
+__device__ __forceinline__ void build_zbin(const FsTables* __restrict__ tabs, char* lds) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+#pragma unroll
+    for (uint32_t p0 = 0; p0 < 4u * kZbinTables; p0 += kWavesPerBlock) {
+        const uint32_t p = p0 + w;
+        if (p < 4u * kZbinTables) {  // lane l: entries 4l .. 4l + 3 of 1-KB piece p (as the plain tables)
+            const uint32_t* pb = tabs->zbin_basis[p];
+            uint32_t x = 0;
+#pragma unroll
+            for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
+            const uint32_t x1 = x ^ pb[0];
+            *reinterpret_cast<u32x4*>(lds + kLdsZbinG + 1024u * p + 16u * lane) = u32x4{x, x1, x ^ pb[1], x1 ^ pb[1]};
+        }
+    }
+}
+// Z_k(y0) and Z_k(y1) for k0, k1 multiples of 4 (two independent chains, interleaved): Z_2048 for
+// every 32 blocks past 63, then one step per set bit of the block count (Z_2048 .. Z_128, region A's
+// Z_64) and of the rest (Z_48 / Z_32 / Z_16, Z_12 / Z_8 / Z_4): at most 8 rounds below 4 KB, 11 for a
+// 9000-B frame. A step no lane of the wave needs is skipped.
+__device__ __forceinline__ uint32_t zstep64(const char* lds, uint32_t v) {
+    return lds32(lds, kLdsRegionA + ((v & 0xffu) << 8)) ^ lds32(lds, kLdsRegionA + (((v >> 8) & 0xffu) << 8) + 32u) ^
+           lds32(lds, kLdsRegionA + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kLdsRegionA + ((v >> 24) << 8) + 96u);
+}
+__device__ __forceinline__ void zshift2(const char* lds, uint32_t& y0, uint32_t k0, uint32_t& y1, uint32_t k1) {
+    uint32_t q0 = k0 >> 6, q1 = k1 >> 6;
+    constexpr uint32_t kTop = 2u << (kZbinTables - 1);  // blocks of the widest table
+    while (__ballot(q0 >= 2u * kTop || q1 >= 2u * kTop) != 0) {  // (frames over 4 KB)
+        const uint32_t top = kLdsZbinG + 4096u * (kZbinTables - 1);
+        if (q0 >= 2u * kTop) { y0 = zplain(lds, y0, top); q0 -= kTop; }
+        if (q1 >= 2u * kTop) { y1 = zplain(lds, y1, top); q1 -= kTop; }
+    }
+#pragma unroll
+    for (int i = kZbinTables - 1; i >= 0; --i) {
+        const uint32_t bit = 2u << i;
+        const bool b0 = (q0 & bit) != 0u, b1 = (q1 & bit) != 0u;
+        if (__ballot(b0 || b1) != 0) {
+            const uint32_t t0 = zplain(lds, y0, kLdsZbinG + 4096u * (uint32_t)i);
+            const uint32_t t1 = zplain(lds, y1, kLdsZbinG + 4096u * (uint32_t)i);
+            y0 = b0 ? t0 : y0;
+            y1 = b1 ? t1 : y1;
+        }
+    }
+    if (__ballot(((q0 | q1) & 1u) != 0u) != 0) {
+        const uint32_t t0 = zstep64(lds, y0), t1 = zstep64(lds, y1);
+        y0 = (q0 & 1u) ? t0 : y0;
+        y1 = (q1 & 1u) ? t1 : y1;
+    }
+    const uint32_t r0 = k0 & 63u, r1 = k1 & 63u;
+    if (__ballot((r0 | r1) >= 16u) != 0) {
+        const uint32_t a0 = r0 >= 48u ? kLdsZ48 : r0 >= 32u ? kLdsZ32 : kLdsZ16;
+        const uint32_t a1 = r1 >= 48u ? kLdsZ48 : r1 >= 32u ? kLdsZ32 : kLdsZ16;
+        const uint32_t t0 = zplain(lds, y0, a0), t1 = zplain(lds, y1, a1);
+        y0 = r0 >= 16u ? t0 : y0;
+        y1 = r1 >= 16u ? t1 : y1;
+    }
+    const uint32_t s0 = r0 & 15u, s1 = r1 & 15u;
+    if (__ballot((s0 | s1) != 0u) != 0) {
+        const uint32_t a0 = s0 == 12u ? kLdsZ12 : s0 == 8u ? kLdsZ8 : kLdsZfin;
+        const uint32_t a1 = s1 == 12u ? kLdsZ12 : s1 == 8u ? kLdsZ8 : kLdsZfin;
+        const uint32_t t0 = zplain(lds, y0, a0), t1 = zplain(lds, y1, a1);
+        y0 = s0 ? t0 : y0;
+        y1 = s1 ? t1 : y1;
+    }
+}
+// frame info word: block phase of frame dword 0 | start alignment << 4 | block position of the last
+// dword << 8 | bytes of the last dword << 12
+__device__ __forceinline__ uint32_t head_rows(uint32_t info) {  // head rows after the first: 1 when dword 1 lies in the 2nd block
+    return ((info & 15u) == 15u && ((info >> 4) & 3u) != 0u) ? 1u : 0u;
+}
+// bytes of a dword at byte x of it and after (x <= 0: all, x >= 4: none)
+__device__ __forceinline__ uint32_t from_byte(int x) {
+    return (uint32_t)(0xffffffffull << ((uint32_t)min(max(x, 0), 4) * 8u));
+}
+// Inclusive scan over the wave's 16 groups of a group-uniform value: DPP row shifts by one and two
+// groups inside each 16-lane row, then the rows' totals by readlane.
+__device__ __forceinline__ uint32_t group_scan(uint32_t x, uint32_t lane) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+    const uint32_t t1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+    const uint32_t t2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
+    const uint32_t row = lane >> 4;
+    return x + (row >= 1u ? t0 : 0u) + (row >= 2u ? t1 : 0u) + (row >= 3u ? t2 : 0u);
+}
+__device__ __forceinline__ LaneKeys lane_keys(uint32_t lane) {
+    LaneKeys keys;
+    const uint32_t c = lane & 7u, h = (lane >> 3) & 3u;
+    keys.cvec = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) keys.cvec |= (32u * j + 4u * c) << (8u * j);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t b = (k + h) & 3u;
+        keys.sel[k] = 0x0c0c0000u | ((4u + b) << 8) | b;
+    }
+    return keys;
+}
+
+typedef __attribute__((address_space(1))) const u32x4_a4 gu32x4;
+
+// A segment-kernel tile: the chunk a group streams and the two walks along it: the REFILL walk (the
+// frame of the row being loaded, kRingG rows ahead) and the CONSUME walk (the frame of the row being
+// streamed: its head rows and its segment's last row). The group's own frame lives in LDS (kGFrame).
+struct TileG {
+    uint64_t S;        // the group's frame (the tile's start only: header DMA, posts)
+    uint32_t len;      // (0: a group past the batch end)
+    uint32_t T, L;     // wave-uniform: the tile's blocks, rows (the chunk length)
+    uint32_t v0;       // the chunk [v0, min(v0 + L, T)) of the tile's blocks (empty when v0 >= T)
+    uint32_t vlast;    // the last block a load may address (the chunk's last; 0 for an empty chunk)
+    uint64_t rdelta;   // refill walk: block v of its frame at rdelta + 64 v (+ this lane's 16 B)
+    uint32_t rvend, rk;
+    uint32_t ck, cvs, cvend, cinfo, clast, chd;  // consume walk: rank, blocks [cvs, cvend), info, segment end, head rows
+    __device__ __forceinline__ uint32_t sa() const { return (uint32_t)S & 3u; }
+    __device__ __forceinline__ uint64_t sdw() const { return S >> 2; }
+    __device__ __forceinline__ int ndall() const { return (int)((sa() + len + 3u) >> 2); }
+    __device__ __forceinline__ uint32_t v1() const { return min(v0 + L, T); }
+};
+
+// The tile's geometry (every lane, before any row): blocks, ranks and the frame table, the chunk,
+// and both walks at the chunk's first block.
+__device__ __forceinline__ void tile_geometry_g(TileG& G, uint32_t tile, uint32_t grp, uint32_t gl, uint32_t lane,
+                                                uint32_t n, uint64_t S, uint32_t len,
+                                                const uint8_t* __restrict__ frames, char* lds, uint32_t sc,
+                                                uint32_t fpt) {
+    G.len = (grp < fpt && tile * fpt + grp < n) ? len : 0u;
+    G.S = S;
+    const uint32_t sa = G.sa();
+    const uint32_t nd = G.len >= 4u ? (sa + G.len + 3u) >> 2 : 0u;
+    const uint32_t ph = ((uint32_t)(reinterpret_cast<uint64_t>(frames) >> 2) + (uint32_t)G.sdw()) & 15u;
+    const uint32_t nb = nd ? (ph + nd + 15u) >> 4 : 0u;
+    const uint32_t incl = group_scan(nb, lane);
+    const uint32_t has = nb ? 1u : 0u;
+    const uint32_t rincl = group_scan(has, lane);
+    const uint32_t vs = incl - nb, rank = rincl - has;
+    G.T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    G.L = (G.T + 15u) >> 4;
+    // the tables (this wave's scratch; LDS ops of one wave complete in order)
+    if (lane < 16u) *reinterpret_cast<uint32_t*>(lds + sc + kGVend + 4u * lane) = ~0u;
+    if (lane < 32u) *reinterpret_cast<uint32_t*>(lds + sc + kGMeta + 4u * lane) = ~0u;
+    if (gl == 0u && nb) {
+        const uint32_t e = ((sa + G.len) & 3u) ? ((sa + G.len) & 3u) : 4u;
+        const uint32_t info = ph | (sa << 4) | (((ph + nd - 1u) & 15u) << 8) | (e << 12);
+        const uint64_t delta = reinterpret_cast<uint64_t>(frames) + 4ull * G.sdw() - 4u * ph - 64ull * vs;
+        *reinterpret_cast<u32x4*>(lds + sc + kGFtab + 16u * rank) =
+            u32x4{(uint32_t)delta, (uint32_t)(delta >> 32), vs + nb, info};
+        *reinterpret_cast<uint32_t*>(lds + sc + kGVend + 4u * rank) = vs + nb;
+    }
+    if (gl == 0u)
+        *reinterpret_cast<u32x4*>(lds + sc + kGFrame + 16u * grp) =
+            u32x4{(uint32_t)S, (uint32_t)(S >> 32), G.len, rank | (has << 8)};
+    G.v0 = grp * G.L;
+    const uint32_t v1 = G.v1();
+    const bool empty = G.v0 >= v1;
+    // the rank holding block v0: #{k : vend_k <= v0}
+    uint32_t k0 = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const u32x4 e = *reinterpret_cast<const u32x4*>(lds + sc + kGVend + 16u * j);
+        k0 += (e.x <= G.v0 ? 1u : 0u) + (e.y <= G.v0 ? 1u : 0u) + (e.z <= G.v0 ? 1u : 0u) + (e.w <= G.v0 ? 1u : 0u);
+    }
+    if (empty) k0 = 0u;  // (an empty chunk loads rank 0's first block: a valid address)
+    const u32x4 e0 = *reinterpret_cast<const u32x4*>(lds + sc + kGFtab + 16u * k0);
+    const uint32_t vs0 = k0 ? lds32(lds, sc + kGVend + 4u * (k0 - 1u)) : 0u;
+    G.vlast = empty ? 0u : v1 - 1u;
+    G.rk = k0;
+    G.rdelta = (((uint64_t)e0.y << 32) | e0.x) + 16u * gl;
+    G.rvend = e0.z;
+    G.ck = k0;
+    G.cvs = empty ? ~0u : vs0;
+    G.cvend = e0.z;
+    G.cinfo = e0.w;
+    G.clast = empty ? ~0u : min(e0.z, v1) - 1u;
+    G.chd = empty ? 0u : head_rows(e0.w);
+}
+
+template <uint32_t kOps>
+__global__ void __launch_bounds__(kThreads, 1)
+digest_kernel_g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__ offsets,
+                const uint32_t* __restrict__ lengths, uint32_t n, uint32_t mtu, const FsTables* __restrict__ tabs,
+                uint2* __restrict__ out, uint8_t* __restrict__ status, uint64_t report, uint8_t* wframes, uint32_t tx,
+                uint32_t fpt) {
+    char* lds = g_lds;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR addresses
+    const uint32_t grp = lane >> 2, gl = lane & 3u;
+    const uint32_t gwave = first_tile(wave);
+    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+    fpt = __builtin_amdgcn_readfirstlane(fpt);
+    const uint32_t ntiles = (n + fpt - 1) / fpt;
+    const uint32_t hw = kLdsHdrG + wave * kHdrWaveG;    // this wave's header slots (and parked parse)
+    const uint32_t sc = kLdsWaveG + wave * kGScratch;  // this wave's scratch
+    const LaneKeys keys = lane_keys(lane);
+
+    TileG G;
+    u32x4 pf[kRingG];
+    // the row a refill loads: chunk row r (clamped to the chunk's last block) through the refill walk;
+    // `nx` = the frame table entry of the walk's next rank, read at the start of the row (every row,
+    // so that no branch waits for an LDS read)
+    struct Next {
+        uint64_t delta;
+        uint32_t vend;
+    };
+    auto row_addr = [&](uint32_t r, const Next& nx) __attribute__((always_inline)) -> gu32x4* {
+        const uint32_t vn = min(G.v0 + r, G.vlast);
+        if (vn >= G.rvend) {  // the chunk's next frame (ranks are consecutive)
+            G.rk += 1u;
+            G.rdelta = nx.delta + 16u * gl;
+            G.rvend = nx.vend;
+        }
+        return reinterpret_cast<gu32x4*>(G.rdelta + ((uint64_t)vn << 6));
+    };
+    auto next_entry = [&](uint32_t k) __attribute__((always_inline)) -> Next {
+        const uint32_t e = sc + kGFtab + 16u * min(k + 1u, kFramesPerTile - 1u);
+        return Next{*reinterpret_cast<const uint64_t*>(lds + e), lds32(lds, e + 8u)};
+    };
+    auto prefetch = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < kRingG; ++i) pf[i] = *row_addr((uint32_t)i, next_entry(G.rk));
+    };
+    auto posts_of = [&](bool first_of_grid) __attribute__((always_inline)) -> uint32_t {
+        const bool ask_mixed = (report & kAskMixed) != 0u;
+        const int nd = G.len >= 4u ? G.ndall() : 0;
+        const bool mixed = ask_mixed && mode_b_worthy(nd);
+        return tile_posts<false>(report, G.len, mixed, first_of_grid);
+    };
+
+    // Preamble: the first tile's descriptors while the tables are built in place; geometry; the first
+    // rows; the header DMA; one barrier.
+    uint32_t tile = gwave;
+    FS_RTSTAMP(5);
+    FS_STAMP(0);
+    const bool first = __builtin_amdgcn_readfirstlane(tile) < ntiles;
+    {
+        uint64_t S;
+        uint32_t len;
+        tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
+        build_region_a(tabs, lds);
+        build_zbin(tabs, lds);
+        descriptors_ready<kOps>(S, len);
+        G.L = 0;
+        if (first) tile_geometry_g(G, tile, grp, gl, lane, n, S, len, frames, lds, sc, fpt);
+    }
+    if (first && G.L > 0u) prefetch();
+    bool x4 = false;
+    if (first) x4 = header_dma<true, kSlotG>(G, frames, lds, hw, gl, lane);
+    const uint32_t posts0 = first && report ? posts_of(gwave == 0u) : 0u;
+    tables_landed<kRingG, kSlotG>(first, G.L > 0u, x4);
+    post_tile(report, posts0, lane);  // (after the counted wait, younger than the rows)
+    __builtin_amdgcn_s_barrier();     // tables ready (raw barrier: no release fence, no vmcnt(0) drain)
+    if ((wave >> 3) != 0u) __builtin_amdgcn_s_setprio(1);  // two-level age priority: the SIMD's younger half first
+    FS_STAMP(1);
+
+    while (tile < ntiles) {
+        const bool fvalid = grp < fpt && tile * fpt + grp < n;
+        const bool parser = fvalid && gl == 0u;  // the group's lane 0 parses, finishes and stores
+        uint32_t A[4] = {0u, 0u, 0u, 0u};
+        uint32_t cs = 0u;
+
+        // ---- one row of the chunk from ring slot w: its events, the lean update, the segment's park
+        auto consume = [&](const u32x4& w, uint32_t r, const uint2& cn) __attribute__((always_inline)) {
+            const uint32_t vr = G.v0 + r;
+            const uint32_t hrow = vr - G.cvs;
+            const bool head = hrow <= G.chd;
+            const bool park = vr == G.clast;
+            const bool tail = park && vr + 1u == G.cvend;
+            // the streams past a frame's last dword keep their value: saved before the update
+            uint32_t As[4];
+            if (tail) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) As[j] = A[j];
+            }
+            lean_row(lds, keys, w, A, cs);
+            // The event fixes, after the update (which fed w unmasked; it is linear in w): the bytes
+            // before the frame (head) and past it (tail) XOR-ed back out of the streams and subtracted
+            // from the sum (disjoint byte masks, so sad16 splits), the CRC init XOR-ed in on frame
+            // bytes [0, 4), and the streams past the last dword restored.
+            if (head || park) {
+                if (head) {
+                    const uint32_t ci = G.cinfo;
+                    const int b0 = 4 * (int)(ci & 15u) + (int)((ci >> 4) & 3u) - 64 * (int)hrow - 16 * (int)gl;
+                    int fix = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t k = from_byte(b0 - 4 * j);
+                        const uint32_t junk = w[j] & ~k;
+                        A[j] ^= junk ^ (k & ~from_byte(b0 + 4 - 4 * j));
+                        fix += (int)sad16(junk, 0u);
+                    }
+                    cs -= (uint32_t)fix;
+                }
+                if (tail) {
+                    const uint32_t ci = G.cinfo;
+                    const int eb = 4 * (int)((ci >> 8) & 15u) + (int)((ci >> 12) & 7u) - 16 * (int)gl;
+                    int fix = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t junk = w[j] & from_byte(eb - 4 * j);
+                        A[j] = (eb - 4 * j > 0) ? (A[j] ^ junk) : As[j];
+                        fix += (int)sad16(junk, 0u);
+                    }
+                    cs -= (uint32_t)fix;
+                }
+                if (park) {  // the segment (rank ck, group grp) into slot ck + grp; the streams restart
+                    const uint32_t s = G.ck + grp;
+                    *reinterpret_cast<u32x4*>(lds + park_at(wave, s) + 16u * gl) = u32x4{A[0], A[1], A[2], A[3]};
+                    uint32_t c = (cs & 0xffffu) + (cs >> 16);
+                    c += dpp_quad<kQuadXor1>(c);
+                    c += dpp_quad<kQuadXor2>(c);
+                    if (gl == 0u) {
+                        *reinterpret_cast<uint32_t*>(lds + sc + kGPcs + 8u * s) = c;
+                        *reinterpret_cast<uint32_t*>(lds + sc + kGMeta + 4u * s) = G.ck;
+                    }
+                    A[0] = A[1] = A[2] = A[3] = 0u;
+                    cs = 0u;
+                    if (tail) {  // the chunk's next frame
+                        G.ck += 1u;
+                        G.cvs = G.cvend;
+                        G.cvend = cn.x;
+                        G.cinfo = cn.y;
+                        G.clast = min(cn.x, G.v1()) - 1u;
+                        G.chd = head_rows(cn.y);
+                    } else {  // the chunk's end: no event after it
+                        G.clast = ~0u;
+                        G.cvs = ~0u;
+                        G.chd = 0u;
+                    }
+                }
+            }
+        };
+        auto block = [&](uint32_t r0, auto refill_tag) __attribute__((always_inline)) {
+            constexpr bool kRefill = decltype(refill_tag)::value;
+#pragma unroll
+            for (int i = 0; i < kRingG; ++i) {
+                // both walks' next frame-table entries, read ahead of the row's lookups
+                const uint2 cn = *reinterpret_cast<const uint2*>(
+                    lds + sc + kGFtab + 16u * min(G.ck + 1u, kFramesPerTile - 1u) + 8u);
+                Next rn;
+                if (kRefill) rn = next_entry(G.rk);
+                consume(pf[i], r0 + (uint32_t)i, cn);
+                if (kRefill) pf[i] = *row_addr(r0 + (uint32_t)(i + kRingG), rn);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        // header parse: after the first block of rows; the header DMA was issued behind the tile's
+        // first rows, so vmcnt(kRingG) retires it once the block's refills are the only younger loads
+        auto parse = [&](bool refilled) __attribute__((always_inline)) {
+            if (refilled) __builtin_amdgcn_s_waitcnt(0x0070 | kRingG);
+            else __builtin_amdgcn_s_waitcnt(0x0070);
+            const u32x4 fr = *reinterpret_cast<const u32x4*>(lds + sc + kGFrame + 16u * grp);
+            const uint64_t S = ((uint64_t)fr.y << 32) | fr.x;
+            parse_tile<kOps, kSlotG>(hw, grp, gl, (uint32_t)S & 3u, fr.z, mtu,
+                                     reinterpret_cast<const uint32_t*>(frames + ((S >> 2) << 2)), parser, hw);
+        };
+        using Yes = std::true_type;
+        using No = std::false_type;
+        const uint32_t R = G.L;
+        if (R > (uint32_t)kRingG) {
+            block(0u, Yes());
+            parse(true);
+            uint32_t r0 = kRingG;
+            for (; r0 + kRingG < R; r0 += kRingG) block(r0, Yes());
+            block(r0, No());
+        } else if (R > 0u) {
+            block(0u, No());
+            parse(false);
+        } else {
+            parse(false);  // no rows (every frame of the tile under 4 bytes): rejected by length
+        }
+        FS_STAMP(2);
+
+        // ---- the parked segments: slot s combined by group s mod 16 (both rounds in one pass): to the
+        // frame's last dword for the segment that ends the frame, else to the end of the chunk's last
+        // block and then shifted by the bytes from there to the frame's last dword
+        const uint32_t T = G.T, L = G.L;
+        {
+            uint32_t Y[2], c[2], sh[2];
+            bool used[2];
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t s = grp + 16u * h;
+                const uint32_t k = s < kSegSlots ? lds32(lds, sc + kGMeta + 4u * s) : ~0u;
+                used[h] = k != ~0u;
+                const uint32_t kk = used[h] ? k : 0u;
+                const u32x4 a4 = *reinterpret_cast<const u32x4*>(lds + park_at(wave, s) + 16u * gl);
+                c[h] = lds32(lds, sc + kGPcs + 8u * s);
+                const uint2 ve = *reinterpret_cast<const uint2*>(lds + sc + kGFtab + 16u * kk + 8u);  // {vend, info}
+                const uint32_t v1g = min((s - kk + 1u) * L, T), dblk = ve.x > v1g ? ve.x - v1g : 0u;
+                const int ealign = 15 - (int)((ve.y >> 8) & 15u);
+                const uint32_t Aa[4] = {a4.x, a4.y, a4.z, a4.w};
+                Y[h] = combine_to_end<LayA1>(lds, Aa, dblk ? 0 : ealign, gl);
+                sh[h] = dblk ? 64u * dblk - 4u * (uint32_t)ealign : 0u;
+            }
+            zshift2(lds, Y[0], sh[0], Y[1], sh[1]);
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h)
+                if (used[h] && gl == 0u) *reinterpret_cast<uint2*>(lds + sc + kGPcs + 8u * (grp + 16u * h)) = make_uint2(Y[h], c[h]);
+        }
+        FS_STAMP(3);
+        // ---- the group's lane 0: its frame's segments (slots rank + the chunks of its first and last
+        // block), finish and store
+        if (parser) {
+            const u32x4 fr = *reinterpret_cast<const u32x4*>(lds + sc + kGFrame + 16u * grp);
+            const uint64_t S = ((uint64_t)fr.y << 32) | fr.x;
+            const uint32_t len = fr.z, rank = fr.w & 0xffu;
+            uint32_t Y = 0u, c = 0u;
+            if (fr.w >> 8) {
+                const uint32_t vend = lds32(lds, sc + kGVend + 4u * rank);
+                const uint32_t vs = rank ? lds32(lds, sc + kGVend + 4u * (rank - 1u)) : 0u;
+                const uint32_t f = rank + vs / L, l = min(rank + (vend - 1u) / L, kSegSlots - 1u);
+                for (uint32_t s = f; s <= l; ++s) {
+                    const uint2 rs = *reinterpret_cast<const uint2*>(lds + sc + kGPcs + 8u * s);
+                    Y ^= rs.x;
+                    c += rs.y;
+                }
+            }
+            const uint32_t e = ((uint32_t)S + len) & 3u;
+            finish_frame<kOps>(lds, unpark_parsed<kOps>(lds, hw, grp), S, len, e ? e : 4u, Y, c, frames, wframes,
+                               lengths, tile * fpt + grp, out, status, tx);
+        }
+        FS_STAMP(4);
+        FS_RTSTAMP(6);
+        tile += nwaves;
+        if (tile < ntiles) {  // next tile: descriptors, geometry, row prefetch, header DMA
+            uint64_t S;
+            uint32_t len;
+            tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
+            descriptors_ready<kOps>(S, len);
+            tile_geometry_g(G, tile, grp, gl, lane, n, S, len, frames, lds, sc, fpt);
+            if (G.L > 0u) prefetch();
+            header_dma<true, kSlotG>(G, frames, lds, hw, gl, lane);
+            if (report) post_tile(report, posts_of(false), lane);
+        }
+    }
+}
+
+// =======================================================================================
 // The small-frame kernel (digest_kernel_s, variant 8): ONE LANE PER FRAME,
 // 64 frames per wave, for batches of short frames (the reference's own benchmark sends 47-byte
 // UDP frames, stacks/benchmark_test.go:12-46). The 4-lane kernels spend a 104-KB table image,
@@ -1880,8 +2366,10 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
             mixed = true;
         }
     }
-    // fs_ctx_set_kernel: 2 the mixed-length kernel, 4 the one-pass kernel
-    if (force == 2 || force == 4) mixed = force == 2;
+    // fs_ctx_set_kernel: 2 the mixed-length (segment) kernel, 4 the one-pass kernel, 3 the piece kernel
+    // (digest_kernel_ab, round 5's mixed-length kernel, kept for same-box comparison)
+    if (force == 2 || force == 3 || force == 4) mixed = force != 4;
+    const bool pieces = force == 3;
     // The small-frame kernel (RX digest and FCS verify; a TX fill keeps the 4-lane choice above).
     // The kernels report launches that met a frame longer than kSmallMaxLen (kReportLong), and the
     // 4-lane kernels, when asked (kAskRan), that a launch ran (kReportRan, with the grid's first
@@ -1939,7 +2427,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH(K)                                                                                        \
     hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
-    chosen(small ? 8u : mixed ? 2u : 4u);
+    chosen(small ? 8u : mixed ? (pieces ? 3u : 2u) : 4u);
     if (small) {
         const uint32_t stiles = (n + 63u) / 64u;  // 64 frames (one per lane) per wave
         uint32_t sb = (stiles + kSmallWaves - 1u) / kSmallWaves;
@@ -1954,15 +2442,18 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     }
     switch (op) {
     case FsOp::kDigest:
-        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
+        if (mixed && pieces) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
+        else if (mixed) FS_LAUNCH((digest_kernel_g<kOpsDigest>));
         else FS_LAUNCH((digest_kernel_a<kOpsDigest>));
         break;
     case FsOp::kFill:
-        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
+        if (mixed && pieces) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
+        else if (mixed) FS_LAUNCH((digest_kernel_g<kOpsTx>));
         else FS_LAUNCH((digest_kernel_a<kOpsTx>));
         break;
     case FsOp::kFcs:
-        if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
+        if (mixed && pieces) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
+        else if (mixed) FS_LAUNCH((digest_kernel_g<kOpsFcs>));
         else FS_LAUNCH((digest_kernel_a<kOpsFcs>));
         break;
     }

@@ -224,13 +224,14 @@ class Engine:
             raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
 
     # kernel variants (fs_ctx_set_kernel): results are identical, only the speed differs
-    KERNEL_AUTO, KERNEL_MIXED, KERNEL_ONE_PASS, KERNEL_SMALL = 0, 2, 4, 8
+    KERNEL_AUTO, KERNEL_MIXED, KERNEL_PIECES, KERNEL_ONE_PASS, KERNEL_SMALL = 0, 2, 3, 4, 8
 
     def set_kernel(self, variant: int) -> None:
         """0 (KERNEL_AUTO): automatic (the mixed-length kernel after a batch that had mixed-length
-        tiles, the one-pass kernel otherwise, the small-frame kernel for short-frame traffic); 2 (KERNEL_MIXED): the kernel that splits long frames
-        of mixed-length tiles into pieces; 4 (KERNEL_ONE_PASS): the one-pass kernel (block-aligned
-        rows); 8 (KERNEL_SMALL): the small-frame kernel (one lane per frame) preferred: it runs until a
+        tiles, the one-pass kernel otherwise, the small-frame kernel for short-frame traffic); 2 (KERNEL_MIXED): the
+        segment kernel (a tile's frames cut into equal chunks, one per 4-lane group); 3 (KERNEL_PIECES): round 5's
+        mixed-length kernel, which splits the long frames of mixed-length tiles into pieces; 4 (KERNEL_ONE_PASS):
+        the one-pass kernel (block-aligned rows); 8 (KERNEL_SMALL): the small-frame kernel (one lane per frame) preferred: it runs until a
         launch reports a frame over 128 B, then the automatic choice until short traffic resumes.
         The automatic choice itself moves to the small-frame kernel after 16 launches seen to run
         with no frame over 128 B (include/framesum.h). A TX fill never runs the small-frame kernel.
@@ -243,7 +244,7 @@ class Engine:
         self._check(self.lib.fs_ctx_set_workgroups(self._ctx, int(workgroups)), "fs_ctx_set_workgroups")
 
     def last_kernel(self) -> int:
-        """The variant (2, 4 or 8) this context's latest launch ran (0 before its first launch). With
+        """The variant (2, 3, 4 or 8) this context's latest launch ran (0 before its first launch). With
         variant 0 the first 16 launches run the mixed-length kernel (2); it stays chosen while its
         batches have mixed-length tiles, uniform traffic then moves to the one-pass kernel (4)."""
         v = self.lib.fs_ctx_last_kernel(self._ctx)

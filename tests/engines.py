@@ -1,11 +1,11 @@
 """Engines for the GPU parity columns: every kernel variant a caller can choose (fs_ctx_set_kernel
-0 / 2 / 4 / 8) and, through the test library's fs_test_set_kernel_exact, the small-frame kernel for
+0 / 2 / 3 / 4 / 8) and, through the test library's fs_test_set_kernel_exact, the small-frame kernel for
 every launch (16: what the host-staged path runs for short batches; variant 8 itself leaves that
 kernel once the reports show long frames, so only this column keeps the small-frame kernel's own
 long-frame path under test)."""
 SMALL_EXACT = 16
-VARIANTS = [4, 2, 0, 8, SMALL_EXACT]
-IDS = ["one_pass", "mixed", "auto", "small", "small_exact"]
+VARIANTS = [4, 2, 3, 0, 8, SMALL_EXACT]
+IDS = ["one_pass", "mixed", "pieces", "auto", "small", "small_exact"]
 
 
 def engine_for(variant: int):

@@ -252,3 +252,95 @@ def crc32_model_lane(buf: bytes, S: int, length: int, chains: int = 1) -> int:
         P = (apply(Z4, Ev) ^ Od) if (nd - 1) & 1 else (Ev ^ apply(Z4, Od))
     t = (4 - (E_ & 3)) & 3
     return apply(ZFIN[t], P) ^ 0xFFFFFFFF
+
+
+def crc32_tile_segments(buf: bytes, frames: list[tuple[int, int]], base_phase: int = 0, groups: int = 16,
+                        model_tail_select: bool = True) -> list[int]:
+    """The segment kernel (digest_kernel_g): a tile's frames as BLOCK-ALIGNED 64-B
+    rows (the one-pass kernel's rows), concatenated in frame order (frames of no stream dword left
+    out) and cut into `groups` equal chunks of L = ceil(T / groups) rows; group g streams its chunk
+    [gL, min(gL + L, T)) through one set of 16 streams, crossing frame boundaries:
+      * a frame's head rows (its first block; the second too when dword 1 lies there) get the head
+        mask and the CRC init (the streams are zero there: the previous segment was parked);
+      * a frame's last block keeps the streams past its last dword untouched (the one-pass tail row);
+      * the row that ends a segment (the frame's last block, or the chunk's last row) PARKS the
+        streams as segment (rank k, group g) = slot k + g and restarts them from zero.
+    After the rows every parked segment is combined like a one-pass frame (q = the frame's last
+    dword's block position for its tail segment, 15 for a segment cut by its chunk's end) and
+    shifted by its distance to the frame end (64 dblk - 4 ealign bytes); a frame's register is the
+    XOR of its segments'. Returns the CRC-32 of every frame (zlib's value)."""
+    padded = b"\0" * 64 + bytes(buf) + b"\0" * 136
+
+    def dword(i):
+        return struct.unpack_from("<I", padded, 64 + 4 * i)[0]
+
+    info = []
+    for S, ln in frames:
+        sdw, sa = S >> 2, S & 3
+        nd = ((S + ln + 3) >> 2) - sdw if ln >= 4 else 0
+        ph = (base_phase + sdw) & 15
+        ealign = (16 - ((ph + nd) & 15)) & 15
+        nb = (ph + nd + ealign) >> 4 if nd > 0 else 0
+        te = ((S + ln) & 3) or 4
+        info.append(dict(S=S, ln=ln, sdw=sdw, sa=sa, nd=nd, ph=ph, ealign=ealign, nb=nb, te=te))
+    ranked = [i for i, f in enumerate(info) if f["nb"] > 0]
+    vs, T = [], 0
+    for i in ranked:
+        vs.append(T)
+        T += info[i]["nb"]
+    L = -(-T // groups) if T else 0
+    slots = {}
+    for g in range(groups):
+        v0, v1 = g * L, min(g * L + L, T)
+        A = [[0] * 4 for _ in range(4)]
+        k = 0
+        for v in range(v0, v1):
+            while vs[k] + info[ranked[k]]["nb"] <= v:
+                k += 1
+            f = info[ranked[k]]
+            hm = (0xFFFFFFFF << (8 * f["sa"])) & 0xFFFFFFFF
+            tm = 0xFFFFFFFF if f["te"] == 4 else (1 << (8 * f["te"])) - 1
+            rowdw0 = f["sdw"] - f["ph"] + 16 * (v - vs[k])  # absolute dword of the block's position 0
+            for lane in range(4):
+                for j in range(4):
+                    x = 16 * (v - vs[k]) + 4 * lane + j - f["ph"]  # frame dword
+                    d = dword(rowdw0 + 4 * lane + j)
+                    c = 0
+                    if x < 0:
+                        d = 0
+                    if x == 0:
+                        d &= hm
+                        c = hm
+                    if x == 1:
+                        c = ~hm & 0xFFFFFFFF
+                    if x == f["nd"] - 1:
+                        d &= tm
+                    if x < f["nd"] or not model_tail_select:
+                        A[lane][j] = apply(Z64, A[lane][j]) ^ d ^ c
+            vend = vs[k] + f["nb"]
+            if v == min(vend, v1) - 1:
+                assert k + g not in slots
+                slots[k + g] = (k, [a[:] for a in A], vend - 1 - v)
+                A = [[0] * 4 for _ in range(4)]
+    assert len(slots) <= len(ranked) + groups - 1 and all(s < len(ranked) + groups - 1 for s in slots)
+    Yk = [0] * len(ranked)
+    for s, (k, A, dblk) in slots.items():
+        f = info[ranked[k]]
+        q = 15 - f["ealign"] if dblk == 0 else 15
+        y = 0
+        for lane in range(4):
+            for j in range(4):
+                p = 4 * lane + j
+                y ^= zero_shift(A[lane][j], 4 * ((q - p) % 16))
+        if dblk:
+            y = zero_shift(y, 64 * dblk - 4 * f["ealign"])
+        Yk[k] ^= y
+    out = []
+    for i, f in enumerate(info):
+        if f["nb"] == 0:
+            out.append(crc32_model(buf, f["S"], f["ln"]))
+            continue
+        Y = Yk[ranked.index(i)]
+        t = (4 - ((f["S"] + f["ln"]) & 3)) & 3
+        out.append(apply(ZFIN[t], Y) ^ 0xFFFFFFFF)
+    return out

@@ -493,17 +493,18 @@ def test_auto_choice_first_launches():
 
 
 def test_set_kernel_accepts_shipped_variants_only():
-    """fs_ctx_set_kernel: 0 (automatic), 2 (mixed-length), 4 (one-pass) and 8 (small-frame) only
-    (the losing variants were removed from the library)."""
+    """fs_ctx_set_kernel: 0 (automatic), 2 (mixed-length: the segment kernel), 3 (round 5's piece
+    kernel), 4 (one-pass) and 8 (small-frame) only (the losing variants
+    were removed from the library)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from seqs_amd import FramesumError
 
     e = Engine(0)
     try:
-        for v in (0, 2, 4, 8):
+        for v in (0, 2, 3, 4, 8):
             e.set_kernel(v)
-        for v in (-1, 1, 3, 5, 6, 7, 9):
+        for v in (-1, 1, 5, 6, 7, 9):
             with pytest.raises(FramesumError, match="variant"):
                 e.set_kernel(v)
     finally:

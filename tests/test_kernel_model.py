@@ -102,3 +102,31 @@ def test_lane_per_frame_crc_vs_zlib():
             want = zlib.crc32(buf[S:S + length])
             for chains in (1, 2):
                 assert crc32_model_lane(buf, S, length, chains) == want, (S, length, chains)
+
+
+def test_tile_segments_vs_zlib():
+    """The segment kernel's decomposition (km.crc32_tile_segments): random tiles of mixed lengths
+    (empty and sub-4-byte frames, gaps, every start alignment and block phase, 1 to 16 groups), the
+    C3 tile (64/576/1500/9000 B), and a tile of 64-B frames beside a jumbo frame; and the tail select
+    is needed (without it every frame of the C3 tile is wrong)."""
+    rnd = random.Random(21)
+    for _ in range(60):
+        n = rnd.choice([1, 2, 3, 5, 16])
+        lens = [rnd.choice([0, 1, 3, 4, 5, 7, 20, 63, 64, 65, 70, 130, 200, 577, 1000]) for _ in range(n)]
+        buf = rnd.randbytes(sum(lens) + 4 * n + 64)
+        frames, o = [], rnd.randrange(4)
+        for ln in lens:
+            frames.append((o, ln))
+            o += ln + rnd.randrange(4)
+        got = km.crc32_tile_segments(buf, frames, rnd.randrange(16), groups=rnd.choice([1, 2, 4, 16]))
+        assert got == [zlib.crc32(buf[S:S + ln]) for S, ln in frames]
+    buf = rnd.randbytes(50000)
+    for lens in ([64, 576, 1500, 9000] * 4, [64] * 15 + [9000]):
+        frames, o = [], 0
+        for ln in lens:
+            frames.append((o, ln))
+            o += ln
+        exp = [zlib.crc32(buf[S:S + ln]) for S, ln in frames]
+        assert km.crc32_tile_segments(buf, frames, 3) == exp
+    bad = km.crc32_tile_segments(buf, frames, 3, model_tail_select=False)
+    assert sum(g != e for g, e in zip(bad, exp)) > 0

@@ -537,6 +537,89 @@ __global__ void __launch_bounds__(1024) k_c3segc(const uint8_t* __restrict__ bas
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+
+// `span16`: the contiguous-span decomposition at the occupancy the 4-lane
+// kernel runs at. A wave owns 16 consecutive frames (a contiguous span: C2's 65,536 frames are 4,096
+// spans, one per wave at 16 waves per CU); the span streams as 1-KB rows (64 lanes x 16 B, a ring of
+// PF rows). Per row each lane folds its 16 B with INDEPENDENT lookups, U = Z12(d0) ^ Z8(d1) ^ Z4(d2)
+// ^ d3 (12 lookups in one round, not a 3-deep Z4 chain), plus 4 v_sad_u16; the 4 lanes of a 64-B
+// block combine by a 2-round tree (Z16 across lane pairs, Z32 across the pairs, by DPP) and lane 3
+// stores the block's (value, sum) partial (global scratch, L2-resident); phase 2, one lane per frame,
+// folds its ~25 block partials with dependent Z64 steps. Tables: plain [4][256] byte tables (Z12, Z8,
+// Z4, Z16, Z32, Z64: 24 KB) replicated REP times (REP 1: unreplicated, bank conflicts as the data
+// falls; REP 2: lane half h reads copy h), so a 1024-thread workgroup fits a CU with room to spare.
+// Random table contents, results not checked: the read pattern with the decomposition's work.
+template <int REP>
+__device__ __forceinline__ uint32_t s16_z(const char* lds, uint32_t t, uint32_t a, uint32_t lane) {
+    const uint32_t base = t * 4096u * REP + (REP > 1 ? ((lane >> 5) & (REP - 1)) * 4096u : 0u);
+    const uint32_t* T = reinterpret_cast<const uint32_t*>(lds + base);
+    return span_xor3(T[a & 0xffu], T[256 + ((a >> 8) & 0xffu)], T[512 + ((a >> 16) & 0xffu)]) ^ T[768 + (a >> 24)];
+}
+template <int PF, int REP>
+__global__ void __launch_bounds__(1024) k_span16(const uint8_t* __restrict__ base, uint32_t nframes, uint32_t flen,
+                                                 uint2* __restrict__ part, uint32_t* out) {
+    __shared__ __attribute__((aligned(16))) char lds[6 * 4096 * REP];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    for (uint32_t o = threadIdx.x * 16u; o < 6u * 4096u * REP; o += 1024u * 16u)
+        *reinterpret_cast<u32x4*>(lds + o) = u32x4{o * 0x9E3779B1u, o ^ 0x5bd1e995u, o * 7u, ~o};
+    __syncthreads();
+    const uint32_t span = wave * gridDim.x + blockIdx.x;  // wave-major, as the kernel's tiles
+    const uint32_t f0 = span * 16u;
+    if (f0 >= nframes) return;
+    const uint32_t nf = min(16u, nframes - f0);
+    const uint64_t s0 = (uint64_t)f0 * flen, s1 = (uint64_t)(f0 + nf) * flen;
+    const uint64_t b0 = s0 & ~uint64_t(63), bytes = ((s1 + 63) & ~uint64_t(63)) - b0;
+    const int rows = (int)((bytes + 1023) / 1024);
+    const u32x4* rp = reinterpret_cast<const u32x4*>(base + b0) + lane;
+    const uint32_t nblk = (uint32_t)(bytes / 64);
+    uint2* wpart = part + (size_t)span * 512u;
+    uint32_t acc = 0;
+    u32x4 pf[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) pf[i] = rp[64 * min(i, rows - 1)];
+    for (int r0 = 0; r0 < rows; r0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int r = r0 + i;
+            const u32x4 v = pf[i];
+            pf[i] = rp[64 * min(r + PF, rows - 1)];
+            const uint32_t u = span_xor3(s16_z<REP>(lds, 0, v.x, lane), s16_z<REP>(lds, 1, v.y, lane),
+                                         s16_z<REP>(lds, 2, v.z, lane)) ^ v.w;
+            uint32_t cs = __builtin_amdgcn_sad_u16(v.x, 0u, 0u);
+            cs = __builtin_amdgcn_sad_u16(v.y, 0u, cs);
+            cs = __builtin_amdgcn_sad_u16(v.z, 0u, cs);
+            cs = __builtin_amdgcn_sad_u16(v.w, 0u, cs);
+            const uint32_t t = s16_z<REP>(lds, 3, u, lane);
+            const uint32_t pr = u ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0xA0, 0xf, 0xf, false);  // [0,0,2,2]
+            const uint32_t q = s16_z<REP>(lds, 4, pr, lane);
+            const uint32_t y = pr ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0x55, 0xf, 0xf, false);  // [1,1,1,1]
+            cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0xB1, 0xf, 0xf, false);
+            cs += (uint32_t)__builtin_amdgcn_mov_dpp((int)cs, 0x4E, 0xf, 0xf, false);
+            const uint32_t blk = (uint32_t)r * 16u + (lane >> 2);
+            if ((lane & 3u) == 3u && blk < nblk) wpart[blk] = make_uint2(y, cs);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (lane < nf) {  // phase 2: one lane per frame, dependent Z64 steps over its blocks
+        const uint64_t fs = (uint64_t)(f0 + lane) * flen, fe = fs + flen;
+        const uint32_t k0 = (uint32_t)((fs - b0) / 64), k1 = (uint32_t)((fe - 1 - b0) / 64);
+        uint32_t y = 0, sum = 0;
+        for (uint32_t k = k0; k <= k1; k += 8) {
+            uint2 pv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pv[j] = wpart[min(k + j, k1)];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (k + j <= k1) {
+                    y = s16_z<REP>(lds, 5, y, lane) ^ pv[j].x;
+                    sum += pv[j].y;
+                }
+        }
+        acc = y ^ sum;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     // `dir [flen]`: forward-only (AL 2) against alternating-direction (AL 3) whole blocks
     const bool dir = argc > 1 && std::string(argv[1]).rfind("dir", 0) == 0;
@@ -693,6 +776,25 @@ int main(int argc, char** argv) {
             run3([&](int i, hipStream_t s) {
                 hipLaunchKernelGGL((k_c3seg<6, 16, 24>), dim3(cus), dim3(1024), 0, s, c3[i % 4], n3, out);
             }, "segments PF=6, drained every 24 rows");
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "span16") {
+        uint2* part;
+        const uint32_t nspans = (nf + 15) / 16;
+        CHECK(hipMalloc(&part, (size_t)nspans * 512 * sizeof(uint2)));
+#define SPAN16(PF, REP)                                                                                    \
+    run([&](int i, hipStream_t s) {                                                                       \
+        hipLaunchKernelGGL((k_span16<PF, REP>), dim3((nspans + 15) / 16), dim3(1024), 0, s, bufs[i % NB], nf, \
+                           flen, part, out);                                                              \
+    }, "span16 PF=" #PF " REP=" #REP)
+        for (int rep = 0; rep < 2; ++rep) {
+            STREAM(4, 16, 1);
+            TILES(4, 5, 2, 16);
+            SPAN16(4, 1);
+            SPAN16(6, 1);
+            SPAN16(4, 2);
+            SPAN16(6, 2);
         }
         return 0;
     }
