@@ -244,11 +244,13 @@ hipError_t launch(fs_ctx* ctx, const uint8_t* frames, const uint64_t* offsets, c
 // automatic choice between the 4-lane kernels. (A device-resident batch's lengths are in device
 // memory: there launch_digest chooses from the kernels' reports.)
 constexpr uint32_t kSmallAutoMaxLen = framesum::kSmallMaxLen;
-int host_force(const fs_ctx* ctx, uint32_t max_len) {
+int host_force(const fs_ctx* ctx, uint32_t max_len, uint32_t min_len) {
     if (ctx->force_kernel != 0 && ctx->force_kernel != 8) return ctx->force_kernel;
+    if (max_len <= kSmallAutoMaxLen) return framesum::kForceSmallExact;
     // a longer frame: the 4-lane choice, never the small-frame kernel, even after a
-    // streak of short device-resident launches
-    return max_len <= kSmallAutoMaxLen ? framesum::kForceSmallExact : framesum::kForceNoSmall;
+    // streak of short device-resident launches; lengths within kUniformSpan: the one-pass kernel from
+    // the first call (a short-lived RecvEthBatch context)
+    return max_len - min_len < framesum::kUniformSpan ? framesum::kForceUniformHost : framesum::kForceNoSmall;
 }
 
 }  // namespace
@@ -534,7 +536,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
             if (sc.bad < n)
                 return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
             const void* df = sc.hi > sc.lo ? mapped(const_cast<uint8_t*>(frames + sc.lo), sc.hi - sc.lo) : nullptr;
-            if (df && host_force(ctx, sc.max_len) == framesum::kForceSmallExact &&
+            if (df && host_force(ctx, sc.max_len, sc.min_len) == framesum::kForceSmallExact &&
                 (reinterpret_cast<uintptr_t>(frames) & 3u) == 0u)
                 return host_inplace(ctx, static_cast<const uint8_t*>(df) - sc.lo, static_cast<const uint64_t*>(dof),
                                     static_cast<const uint32_t*>(dln), n, mtu, out, status);
@@ -572,7 +574,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
             drain_host_streams(ctx);  // the descriptor copy reads the caller's arrays: done before returning
             return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
         }
-        const int force = host_force(ctx, sc.max_len);
+        const int force = host_force(ctx, sc.max_len, sc.min_len);
         if (sc.hi - sc.lo <= kChunkBytes)
             return host_single(ctx, frames, frames_bytes, offsets, lengths, n, mtu, out, status, sc, force);
         FS_HIP(ctx, hipStreamSynchronize(ks));  // (the chunked path below stages the descriptors itself)
@@ -581,7 +583,7 @@ fs_status fs_digest_batch_host(fs_ctx* ctx, const uint8_t* frames, uint64_t fram
         framesum::plan::scan_from(scan_descriptors(offsets, lengths, n), offsets, lengths, n, frames_bytes);
     if (sc.bad < n)
         return set_err(ctx, FS_E_INVALID, "fs_digest_batch_host: frame " + std::to_string(sc.bad) + " ends past frames_bytes");
-    const int force = host_force(ctx, sc.max_len);
+    const int force = host_force(ctx, sc.max_len, sc.min_len);
     ctx->host_dirty = true;  // until this call has waited for all of its work
     ctx->last_host_path = 3;
     pst = ensure_pinned(ctx, n);

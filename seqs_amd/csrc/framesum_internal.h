@@ -32,12 +32,7 @@ struct FsTables {
     // T[b][1 << j] of the 40 plain [4][256] tables above, in LDS-image order (piece p = 4 t + b is the
     // 1-KB piece at LDS byte 1024 p): the kernels build them in place by VALU, as region A
     uint32_t plain_basis[40][8];
-    // The segment kernel's binary shift tables Z_128, Z_256, ..., Z_2048 ([4][256] each, 20 1-KB pieces
-    // after its scratch in LDS; built in place from these bases like the plain tables): a segment's
-    // value is shifted to its frame's end in at most ~10 lookup rounds
-    uint32_t zbin_basis[20][8];
 };
-constexpr int kZbinTables = 5;  // Z_(128 << i), i = 0..4
 constexpr uint32_t kTablesLdsBytes = 65536 + 4096 * 10;  // the LDS image: everything before z64_basis
 static_assert(offsetof(FsTables, z64_basis) == kTablesLdsBytes, "FsTables layout");
 static_assert(offsetof(FsTables, z32) == 65536 && offsetof(FsTables, plain_basis) == kTablesLdsBytes + 128,
@@ -94,6 +89,12 @@ constexpr uint32_t kShortLaunchesAuto = 16, kShortLaunchesSmall = 2;
 // kernel would stream that frame with one lane)
 constexpr int kForceSmallExact = 16;
 constexpr int kForceNoSmall = 17;
+// ... and for a host batch whose lengths all lie within kUniformSpan bytes (no tile can differ by the
+// 4 rows a mixed-length tile needs), the one-pass kernel from the context's first call: the initial
+// mixed-kernel window (kInitialMixedLaunches) is for device-resident batches, whose lengths the host
+// never sees
+constexpr int kForceUniformHost = 18;
+constexpr uint32_t kUniformSpan = 256;
 hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
                          uint32_t mtu, const FsTables* tables, void* out, uint8_t* status, hipStream_t stream,
                          int num_cus, volatile uint32_t* report_host, uint32_t* report_dev, uint32_t* next_id,

@@ -1663,7 +1663,7 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
 
 
 // =======================================================================================
-// The SEGMENT kernel (digest_kernel_g, variant 2 since round 6): mixed lengths on
+// The SEGMENT kernel (digest_kernel_g, variant 3, round 6): mixed lengths on
 // the one-pass kernel's block-aligned rows, with no idle group and no pass. A tile's frames, as the
 // 64-B blocks that hold them, are concatenated in frame order (a frame with no stream dword takes no
 // block; the others are numbered by RANK) into T virtual blocks, cut into 16 CHUNKS of
@@ -1702,73 +1702,6 @@ static_assert(kGPcs - kGVend >= 4u * kFramesPerTile && kGMeta - kGPcs >= 8u * (k
 // reads): wave w owns entries 16 w .. 16 w + 15, two 64-B slots each.
 __device__ __forceinline__ uint32_t park_at(uint32_t wave, uint32_t s) {
     return kLdsRegionA + (16u * wave + (s >> 1)) * 256u + 128u + 64u * (s & 1u);
-}
-// The binary shift tables Z_128 .. Z_2048 after the scratch (FsTables::zbin_basis), built in place
-constexpr uint32_t kLdsZbinG = kLdsWaveG + kWavesPerBlock * kGScratch;
-static_assert(kLdsZbinG + 4096u * kZbinTables <= kLdsBytes, "segment kernel shift tables");
-__device__ __forceinline__ void build_zbin(const FsTables* __restrict__ tabs, char* lds) {
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-#pragma unroll
-    for (uint32_t p0 = 0; p0 < 4u * kZbinTables; p0 += kWavesPerBlock) {
-        const uint32_t p = p0 + w;
-        if (p < 4u * kZbinTables) {  // lane l: entries 4l .. 4l + 3 of 1-KB piece p (as the plain tables)
-            const uint32_t* pb = tabs->zbin_basis[p];
-            uint32_t x = 0;
-#pragma unroll
-            for (uint32_t j = 2; j < 8; ++j) x ^= pb[j] & (0u - ((lane >> (j - 2u)) & 1u));
-            const uint32_t x1 = x ^ pb[0];
-            *reinterpret_cast<u32x4*>(lds + kLdsZbinG + 1024u * p + 16u * lane) = u32x4{x, x1, x ^ pb[1], x1 ^ pb[1]};
-        }
-    }
-}
-// Z_k(y0) and Z_k(y1) for k0, k1 multiples of 4 (two independent chains, interleaved): Z_2048 for
-// every 32 blocks past 63, then one step per set bit of the block count (Z_2048 .. Z_128, region A's
-// Z_64) and of the rest (Z_48 / Z_32 / Z_16, Z_12 / Z_8 / Z_4): at most 8 rounds below 4 KB, 11 for a
-// 9000-B frame. A step no lane of the wave needs is skipped.
-__device__ __forceinline__ uint32_t zstep64(const char* lds, uint32_t v) {
-    return lds32(lds, kLdsRegionA + ((v & 0xffu) << 8)) ^ lds32(lds, kLdsRegionA + (((v >> 8) & 0xffu) << 8) + 32u) ^
-           lds32(lds, kLdsRegionA + (((v >> 16) & 0xffu) << 8) + 64u) ^ lds32(lds, kLdsRegionA + ((v >> 24) << 8) + 96u);
-}
-__device__ __forceinline__ void zshift2(const char* lds, uint32_t& y0, uint32_t k0, uint32_t& y1, uint32_t k1) {
-    uint32_t q0 = k0 >> 6, q1 = k1 >> 6;
-    constexpr uint32_t kTop = 2u << (kZbinTables - 1);  // blocks of the widest table
-    while (__ballot(q0 >= 2u * kTop || q1 >= 2u * kTop) != 0) {  // (frames over 4 KB)
-        const uint32_t top = kLdsZbinG + 4096u * (kZbinTables - 1);
-        if (q0 >= 2u * kTop) { y0 = zplain(lds, y0, top); q0 -= kTop; }
-        if (q1 >= 2u * kTop) { y1 = zplain(lds, y1, top); q1 -= kTop; }
-    }
-#pragma unroll
-    for (int i = kZbinTables - 1; i >= 0; --i) {
-        const uint32_t bit = 2u << i;
-        const bool b0 = (q0 & bit) != 0u, b1 = (q1 & bit) != 0u;
-        if (__ballot(b0 || b1) != 0) {
-            const uint32_t t0 = zplain(lds, y0, kLdsZbinG + 4096u * (uint32_t)i);
-            const uint32_t t1 = zplain(lds, y1, kLdsZbinG + 4096u * (uint32_t)i);
-            y0 = b0 ? t0 : y0;
-            y1 = b1 ? t1 : y1;
-        }
-    }
-    if (__ballot(((q0 | q1) & 1u) != 0u) != 0) {
-        const uint32_t t0 = zstep64(lds, y0), t1 = zstep64(lds, y1);
-        y0 = (q0 & 1u) ? t0 : y0;
-        y1 = (q1 & 1u) ? t1 : y1;
-    }
-    const uint32_t r0 = k0 & 63u, r1 = k1 & 63u;
-    if (__ballot((r0 | r1) >= 16u) != 0) {
-        const uint32_t a0 = r0 >= 48u ? kLdsZ48 : r0 >= 32u ? kLdsZ32 : kLdsZ16;
-        const uint32_t a1 = r1 >= 48u ? kLdsZ48 : r1 >= 32u ? kLdsZ32 : kLdsZ16;
-        const uint32_t t0 = zplain(lds, y0, a0), t1 = zplain(lds, y1, a1);
-        y0 = r0 >= 16u ? t0 : y0;
-        y1 = r1 >= 16u ? t1 : y1;
-    }
-    const uint32_t s0 = r0 & 15u, s1 = r1 & 15u;
-    if (__ballot((s0 | s1) != 0u) != 0) {
-        const uint32_t a0 = s0 == 12u ? kLdsZ12 : s0 == 8u ? kLdsZ8 : kLdsZfin;
-        const uint32_t a1 = s1 == 12u ? kLdsZ12 : s1 == 8u ? kLdsZ8 : kLdsZfin;
-        const uint32_t t0 = zplain(lds, y0, a0), t1 = zplain(lds, y1, a1);
-        y0 = s0 ? t0 : y0;
-        y1 = s1 ? t1 : y1;
-    }
 }
 // frame info word: block phase of frame dword 0 | start alignment << 4 | block position of the last
 // dword << 8 | bytes of the last dword << 12
@@ -1943,7 +1876,6 @@ digest_kernel_g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         uint32_t len;
         tile_descriptors(tile, grp, n, offsets, lengths, S, len, fpt);
         build_region_a(tabs, lds);
-        build_zbin(tabs, lds);
         descriptors_ready<kOps>(S, len);
         G.L = 0;
         if (first) tile_geometry_g(G, tile, grp, gl, lane, n, S, len, frames, lds, sc, fpt);
@@ -2080,28 +2012,21 @@ digest_kernel_g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         // frame's last dword for the segment that ends the frame, else to the end of the chunk's last
         // block and then shifted by the bytes from there to the frame's last dword
         const uint32_t T = G.T, L = G.L;
-        {
-            uint32_t Y[2], c[2], sh[2];
-            bool used[2];
 #pragma unroll
-            for (uint32_t h = 0; h < 2; ++h) {
-                const uint32_t s = grp + 16u * h;
-                const uint32_t k = s < kSegSlots ? lds32(lds, sc + kGMeta + 4u * s) : ~0u;
-                used[h] = k != ~0u;
-                const uint32_t kk = used[h] ? k : 0u;
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t s = grp + 16u * h;
+            const uint32_t k = s < kSegSlots ? lds32(lds, sc + kGMeta + 4u * s) : ~0u;
+            if (k != ~0u) {
                 const u32x4 a4 = *reinterpret_cast<const u32x4*>(lds + park_at(wave, s) + 16u * gl);
-                c[h] = lds32(lds, sc + kGPcs + 8u * s);
-                const uint2 ve = *reinterpret_cast<const uint2*>(lds + sc + kGFtab + 16u * kk + 8u);  // {vend, info}
-                const uint32_t v1g = min((s - kk + 1u) * L, T), dblk = ve.x > v1g ? ve.x - v1g : 0u;
+                const uint32_t c = lds32(lds, sc + kGPcs + 8u * s);
+                const uint2 ve = *reinterpret_cast<const uint2*>(lds + sc + kGFtab + 16u * k + 8u);  // {vend, info}
+                const uint32_t v1g = min((s - k + 1u) * L, T), dblk = ve.x > v1g ? ve.x - v1g : 0u;
                 const int ealign = 15 - (int)((ve.y >> 8) & 15u);
                 const uint32_t Aa[4] = {a4.x, a4.y, a4.z, a4.w};
-                Y[h] = combine_to_end<LayA1>(lds, Aa, dblk ? 0 : ealign, gl);
-                sh[h] = dblk ? 64u * dblk - 4u * (uint32_t)ealign : 0u;
+                uint32_t Y = combine_to_end<LayA1>(lds, Aa, dblk ? 0 : ealign, gl);
+                if (dblk) Y = zshift(lds, Y, 64u * dblk - 4u * (uint32_t)ealign);
+                if (gl == 0u) *reinterpret_cast<uint2*>(lds + sc + kGPcs + 8u * s) = make_uint2(Y, c);
             }
-            zshift2(lds, Y[0], sh[0], Y[1], sh[1]);
-#pragma unroll
-            for (uint32_t h = 0; h < 2; ++h)
-                if (used[h] && gl == 0u) *reinterpret_cast<uint2*>(lds + sc + kGPcs + 8u * (grp + 16u * h)) = make_uint2(Y[h], c[h]);
         }
         FS_STAMP(3);
         // ---- the group's lane 0: its frame's segments (slots rank + the chunks of its first and last
@@ -2366,10 +2291,11 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
             mixed = true;
         }
     }
-    // fs_ctx_set_kernel: 2 the mixed-length (segment) kernel, 4 the one-pass kernel, 3 the piece kernel
-    // (digest_kernel_ab, round 5's mixed-length kernel, kept for same-box comparison)
+    // fs_ctx_set_kernel: 2 the mixed-length kernel (digest_kernel_ab, pieces), 4 the one-pass kernel, 3 the
+    // segment kernel (digest_kernel_g: another mixed-length decomposition, slower on C3)
     if (force == 2 || force == 3 || force == 4) mixed = force != 4;
-    const bool pieces = force == 3;
+    if (force == kForceUniformHost) mixed = false;
+    const bool segments = force == 3;
     // The small-frame kernel (RX digest and FCS verify; a TX fill keeps the 4-lane choice above).
     // The kernels report launches that met a frame longer than kSmallMaxLen (kReportLong), and the
     // 4-lane kernels, when asked (kAskRan), that a launch ran (kReportRan, with the grid's first
@@ -2383,7 +2309,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     bool small = false;
     // kForceNoSmall (a host-staged batch with a long frame) reports as the automatic choice does, so
     // its long frames end a short streak; it only never picks the small-frame kernel itself
-    const bool autov = force == 0 || force == kForceNoSmall;
+    const bool autov = force == 0 || force == kForceNoSmall || force == kForceUniformHost;
     if (can_report) {
         const uint32_t lng = report_host[kReportLong], rw = report_host[kReportRan], ran = rw & 0xFFFFu;
         const bool ran_new = ran != report_host[kReportRanSeen];
@@ -2408,7 +2334,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
         small = true;  // no report block: the caller's choice as it stands
     }
     if (force == kForceSmallExact) small = true;
-    if (force == kForceNoSmall || op == FsOp::kFill) small = false;
+    if (force == kForceNoSmall || force == kForceUniformHost || op == FsOp::kFill) small = false;
     if (small) mixed = false;
     // the variant this launch runs, for fs_ctx_last_kernel (host-only word)
     auto chosen = [&](uint32_t v) {
@@ -2427,7 +2353,7 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
 #define FS_LAUNCH(K)                                                                                        \
     hipLaunchKernelGGL(K, dim3(blocks), dim3(kThreads), 0, stream, frames, offsets, lengths, n, mtu, \
                        tables, o, status, report, wframes, tx, fpt)
-    chosen(small ? 8u : mixed ? (pieces ? 3u : 2u) : 4u);
+    chosen(small ? 8u : mixed ? (segments ? 3u : 2u) : 4u);
     if (small) {
         const uint32_t stiles = (n + 63u) / 64u;  // 64 frames (one per lane) per wave
         uint32_t sb = (stiles + kSmallWaves - 1u) / kSmallWaves;
@@ -2442,18 +2368,18 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     }
     switch (op) {
     case FsOp::kDigest:
-        if (mixed && pieces) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
-        else if (mixed) FS_LAUNCH((digest_kernel_g<kOpsDigest>));
+        if (mixed && segments) FS_LAUNCH((digest_kernel_g<kOpsDigest>));
+        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsDigest>));
         else FS_LAUNCH((digest_kernel_a<kOpsDigest>));
         break;
     case FsOp::kFill:
-        if (mixed && pieces) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
-        else if (mixed) FS_LAUNCH((digest_kernel_g<kOpsTx>));
+        if (mixed && segments) FS_LAUNCH((digest_kernel_g<kOpsTx>));
+        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsTx>));
         else FS_LAUNCH((digest_kernel_a<kOpsTx>));
         break;
     case FsOp::kFcs:
-        if (mixed && pieces) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
-        else if (mixed) FS_LAUNCH((digest_kernel_g<kOpsFcs>));
+        if (mixed && segments) FS_LAUNCH((digest_kernel_g<kOpsFcs>));
+        else if (mixed) FS_LAUNCH((digest_kernel_ab<kOpsFcs>));
         else FS_LAUNCH((digest_kernel_a<kOpsFcs>));
         break;
     }

@@ -108,20 +108,20 @@ inline uint32_t first_frame_out_of_range(const uint64_t* offsets, const uint32_t
 // short frames walks 65,536 descriptors per call, and two passes of a branchy loop were a sizeable
 // part of its host time. bad = the first out-of-range frame, or n.
 struct Scan {
-    uint32_t bad, max_len;
+    uint32_t bad, max_len, min_len;
     uint64_t lo, hi;
 };
-// The reductions only (min offset, max offset, max end, max length): four independent min/max
-// chains the compiler vectorizes. Every frame lies in range iff max offset <= frames_bytes and
+// The reductions only (min offset, max offset, max end, max and min length): five independent
+// min/max chains the compiler vectorizes. Every frame lies in range iff max offset <= frames_bytes and
 // max end + extra <= frames_bytes, as long as no end wraps (frames_bytes < 2^64 - 2^33: a larger
 // buffer falls back to the per-frame test).
 struct ScanCore {
     uint64_t lo, hi_off, hi_end;
-    uint32_t max_len;
+    uint32_t max_len, min_len;
 };
 inline ScanCore scan_core(const uint64_t* offsets, const uint32_t* lengths, uint32_t n) {
     uint64_t lo = UINT64_MAX, ho = 0, he = 0;
-    uint32_t mx = 0;
+    uint32_t mx = 0, mn = UINT32_MAX;
     for (uint32_t i = 0; i < n; ++i) {
         const uint64_t o = offsets[i];
         const uint32_t l = lengths[i];
@@ -129,12 +129,14 @@ inline ScanCore scan_core(const uint64_t* offsets, const uint32_t* lengths, uint
         ho = o > ho ? o : ho;
         he = o + l > he ? o + l : he;
         mx = l > mx ? l : mx;
+        mn = l < mn ? l : mn;
     }
     ScanCore c;
     c.lo = lo;
     c.hi_off = ho;
     c.hi_end = he;
     c.max_len = mx;
+    c.min_len = n ? mn : 0;
     return c;
 }
 inline Scan scan_from(const ScanCore& c, const uint64_t* offsets, const uint32_t* lengths, uint32_t n,
@@ -145,6 +147,7 @@ inline Scan scan_from(const ScanCore& c, const uint64_t* offsets, const uint32_t
                           frames_bytes - c.hi_end >= extra;
     s.bad = (n == 0 || in_range) ? n : first_frame_out_of_range(offsets, lengths, n, frames_bytes, extra);
     s.max_len = c.max_len;
+    s.min_len = c.min_len;
     s.lo = n ? c.lo : 0;
     s.hi = c.hi_end;
     return s;

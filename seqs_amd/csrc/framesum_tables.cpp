@@ -71,20 +71,6 @@ void build_tables(FsTables* t) {
                 if ((e >> j) & 1u) v ^= t->plain_basis[p][j];
             if (v != plain[256 * p + e]) throw std::logic_error("plain table basis mismatch");
         }
-    // the segment kernel's binary shift tables (bases only: the kernel builds the tables in place)
-    for (int i = 0; i < kZbinTables; ++i) {
-        static uint32_t zb[4][256];
-        op_table(t1, 128 << i, zb);
-        for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t j = 0; j < 8; ++j) t->zbin_basis[4 * i + b][j] = zb[b][1u << j];
-        for (uint32_t b = 0; b < 4; ++b)
-            for (uint32_t e = 0; e < 256; ++e) {
-                uint32_t v = 0;
-                for (uint32_t j = 0; j < 8; ++j)
-                    if ((e >> j) & 1u) v ^= t->zbin_basis[4 * i + b][j];
-                if (v != zb[b][e]) throw std::logic_error("binary shift table basis mismatch");
-            }
-    }
     // The final step Z_(4-t) replaces "Z_4 then undo t appended zero bytes"; Z_1[0] is the
     // standard byte table used for frames shorter than 4 bytes.
     if (std::memcmp(t->zfin[3][0], t1, sizeof(t1)) != 0) throw std::logic_error("Z_1 table mismatch");

@@ -224,14 +224,14 @@ class Engine:
             raise FramesumError(f"{what} failed ({st}): {self.lib.fs_last_error(self._ctx).decode()}")
 
     # kernel variants (fs_ctx_set_kernel): results are identical, only the speed differs
-    KERNEL_AUTO, KERNEL_MIXED, KERNEL_PIECES, KERNEL_ONE_PASS, KERNEL_SMALL = 0, 2, 3, 4, 8
+    KERNEL_AUTO, KERNEL_MIXED, KERNEL_SEGMENTS, KERNEL_ONE_PASS, KERNEL_SMALL = 0, 2, 3, 4, 8
 
     def set_kernel(self, variant: int) -> None:
         """0 (KERNEL_AUTO): automatic (the mixed-length kernel after a batch that had mixed-length
         tiles, the one-pass kernel otherwise, the small-frame kernel for short-frame traffic); 2 (KERNEL_MIXED): the
-        segment kernel (a tile's frames cut into equal chunks, one per 4-lane group); 3 (KERNEL_PIECES): round 5's
-        mixed-length kernel, which splits the long frames of mixed-length tiles into pieces; 4 (KERNEL_ONE_PASS):
-        the one-pass kernel (block-aligned rows); 8 (KERNEL_SMALL): the small-frame kernel (one lane per frame) preferred: it runs until a
+        mixed-length kernel, which splits the long frames of mixed-length tiles into pieces; 3 (KERNEL_SEGMENTS):
+        the segment kernel (a tile's frames cut into equal chunks, one per 4-lane group; slower on C3,
+        DESIGN.md §3.14); 4 (KERNEL_ONE_PASS): the one-pass kernel (block-aligned rows); 8 (KERNEL_SMALL): the small-frame kernel (one lane per frame) preferred: it runs until a
         launch reports a frame over 128 B, then the automatic choice until short traffic resumes.
         The automatic choice itself moves to the small-frame kernel after 16 launches seen to run
         with no frame over 128 B (include/framesum.h). A TX fill never runs the small-frame kernel.

@@ -5,7 +5,7 @@ kernel once the reports show long frames, so only this column keeps the small-fr
 long-frame path under test)."""
 SMALL_EXACT = 16
 VARIANTS = [4, 2, 3, 0, 8, SMALL_EXACT]
-IDS = ["one_pass", "mixed", "pieces", "auto", "small", "small_exact"]
+IDS = ["one_pass", "mixed", "segments", "auto", "small", "small_exact"]
 
 
 def engine_for(variant: int):

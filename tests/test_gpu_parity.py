@@ -492,9 +492,41 @@ def test_auto_choice_first_launches():
         e.close()
 
 
+def test_host_first_call_kernel_choice():
+    """a fresh context's FIRST host-staged call (what a short-lived Go
+    RecvEthBatch context makes) runs the one-pass kernel when the batch's lengths lie within 256 B of
+    each other (no tile can be mixed), and the mixed-length kernel when they do not; bit-exact
+    against the oracle either way. (Device-resident batches keep the initial mixed window: their
+    lengths are in device memory.)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    for label, (b, o, l), expect in (
+            ("uniform 1500 B", synth.uniform_batch(2048, 1500, seed=61), Engine.KERNEL_ONE_PASS),
+            ("uniform 576..800 B", (None, None, None), Engine.KERNEL_ONE_PASS),
+            ("mixed C3", synth.mixed_batch(2048, seed=62), Engine.KERNEL_MIXED)):
+        if b is None:  # valid TCP frames of 576..800 B at every start alignment
+            import random
+
+            import framegen
+            rnd = random.Random(63)
+            frames = [framegen.valid_frame(rnd, payload=rnd.randrange(522, 747)) for _ in range(1500)]
+            b, o, l = pack_frames(frames, align=1)
+            assert 576 <= int(l.min()) and int(l.max()) <= 800
+        e = Engine(0)
+        try:
+            dig, st = e.digest_host(b, o, l)
+            assert e.last_kernel() == expect, (label, e.last_kernel())
+            edig, est = coracle.digest_batch(b, o, l, nthreads=8)
+            for f in ("crc32", "ip_csum", "l4_csum"):
+                assert np.array_equal(dig[f], edig[f]), (label, f)
+            assert np.array_equal(st, est), label
+        finally:
+            e.close()
+
+
 def test_set_kernel_accepts_shipped_variants_only():
-    """fs_ctx_set_kernel: 0 (automatic), 2 (mixed-length: the segment kernel), 3 (round 5's piece
-    kernel), 4 (one-pass) and 8 (small-frame) only (the losing variants
+    """fs_ctx_set_kernel: 0 (automatic), 2 (mixed-length: pieces), 3 (the segment kernel), 4 (one-pass)
+    and 8 (small-frame) only (the losing variants
     were removed from the library)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
