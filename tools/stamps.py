@@ -16,19 +16,34 @@ p = argparse.ArgumentParser()
 p.add_argument("--config", default="c2")
 p.add_argument("--frames", type=int, default=65536)
 p.add_argument("--kernel", type=int, default=0)
+p.add_argument("--op", choices=["digest", "fill"], default="digest",
+               help="fill: fs_fill_batch (FS_FILL_CSUM|FS_FCS_APPEND) on C2 frames with 4 spare bytes each")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 bs = []
 for b in range(4):
     buf, off, ln = (synth.uniform_batch(a.frames, 1500, seed=1 + b) if a.config == "c2"
                     else synth.mixed_batch(a.frames, seed=2 + b))
+    if a.op == "fill":  # 4 spare bytes after every frame (the FCS), 4-byte aligned (as tools/prof_driver.py)
+        step = (ln.astype(np.int64) + 4 + 3) // 4 * 4
+        noff = np.zeros_like(off)
+        noff[1:] = np.cumsum(step[:-1])
+        nbuf = np.zeros(int(noff[-1] + step[-1]) + 16, np.uint8)
+        for i in range(0, len(ln), 4096):  # (block copies: frames are contiguous in both layouts)
+            j = min(len(ln), i + 4096)
+            for k in range(i, j):
+                nbuf[noff[k]:noff[k] + ln[k]] = buf[off[k]:off[k] + ln[k]]
+        buf, off = nbuf, noff
     bs.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)))
 e = Engine(0)
 e.set_kernel(a.kernel)
 out = torch.empty((a.frames, 2), dtype=torch.int32, device=dev)
 st = torch.empty((a.frames,), dtype=torch.uint8, device=dev)
 for i in range(8 if a.kernel else 40):  # (variant 0: past the automatic choice's initial window)
-    e.digest_device(*bs[i % 4], out=out, status=st)
+    if a.op == "fill":
+        e.fill_device(*bs[i % 4], flags=3, out=out, status=st)
+    else:
+        e.digest_device(*bs[i % 4], out=out, status=st)
 torch.cuda.synchronize()
 arr = np.zeros(8192 * 16, dtype=np.uint64)
 rc = e.lib.fs_debug_read_stamps(arr.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(arr.nbytes))
