@@ -68,6 +68,10 @@ constexpr uint32_t kInitialMixedLaunches = 16;
 constexpr int kReportLong = 5, kReportRan = 6, kReportLongSeen = 7, kReportRanSeen = 8, kReportShort = 9;
 constexpr int kReportLongEver = 10;
 constexpr uint32_t kReportRanLong = 1u << 16;
+// ... and in the kReportLatest word, the posting tile held a frame longer than the mixed-length kernel's
+// pieces cover (kMaxFullPasses passes of 16 pieces) beside short ones: the automatic choice then runs
+// the segment kernel (variant 3), which splits any frame into equal chunks
+constexpr uint32_t kReportMixedGiant = 1u << 16;
 constexpr uint32_t kSmallMaxLen = 128;
 // the kernels' `report` argument: the report block's device address in bits 6..46 (host-mapped
 // memory sits below 2^47; the block is 64-B aligned), a watch flag in bit 47, the launch id in bits

@@ -825,21 +825,24 @@ __device__ __forceinline__ void full_piece_unit(Unit& U, const char* lds, const 
              (uint32_t)(kFramesPerTile + q);
 }
 
-// Would the tile run better in mode B? (the decision of tile_geometry, for the mode-A-only
-// kernel's report)
-__device__ __forceinline__ bool mode_b_worthy(int nd) {
+// How the tile's lengths mix (the report that steers the automatic choice): 0 similar lengths (the
+// one-pass kernel), 1 mode B pays (the decision of tile_geometry: the mixed-length kernel), 2 a frame
+// longer than mode B's passes cover beside frames at least 4 rows shorter (the segment kernel).
+constexpr uint32_t kMixNone = 0u, kMixPieces = 1u, kMixGiant = 2u;
+__device__ __forceinline__ uint32_t mixed_class(int nd) {
     const int rows = (nd + kRowDwords - 1) / kRowDwords;
     const int rmax = group_max(rows);
     // a tile whose frames differ by under 4 rows (256 B) has nothing for pieces to fill: the
     // common case of uniform batches skips the piece arithmetic (it only steers the choice)
-    if (rmax + group_max(-rows) < 4) return false;
+    if (rmax + group_max(-rows) < 4) return kMixNone;
     const int RA = (rmax + kPrefetch - 1) / kPrefetch * kPrefetch;
     const int npc = nd > 0 ? pieces_of(nd) : 1;
     const int nd0 = nd - kPieceDwords * (npc - 1);
     const int P0B = (group_max((nd0 + kRowDwords - 1) / kRowDwords) + kPrefetch - 1) / kPrefetch * kPrefetch;
     const int F = group_sum(npc - 1);
     const int fullp = (F + kFramesPerTile - 1) / kFramesPerTile;
-    return F > 0 && fullp <= kMaxFullPasses && P0B + (kPieceRows + 2) * fullp < RA;
+    if (F > 0 && fullp > kMaxFullPasses) return kMixGiant;
+    return F > 0 && P0B + (kPieceRows + 2) * fullp < RA ? kMixPieces : kMixNone;
 }
 
 // ---- the mode-A-only kernel's tile state: the group's own frame and its single pass
@@ -1176,20 +1179,21 @@ __device__ __forceinline__ bool report_watch(uint64_t report) { return ((report 
 // computes them while its rows load and stores them after its counted wait (computing them after the
 // wait put the wave's barrier arrival ~0.1 us later on C2). kMixedOnAsk: mixed tiles are posted only
 // when the launch asks (kAskMixed; the mixed-length kernel).
-constexpr uint32_t kPostMixed = 1u, kPostRan = 2u, kPostRanLong = 4u, kPostLong = 8u;
+constexpr uint32_t kPostMixed = 1u, kPostRan = 2u, kPostRanLong = 4u, kPostLong = 8u, kPostGiant = 16u;
 template <bool kMixedOnAsk>
-__device__ __forceinline__ uint32_t tile_posts(uint64_t report, uint32_t len, bool mixed_tile, bool first_tile_of_grid) {
+__device__ __forceinline__ uint32_t tile_posts(uint64_t report, uint32_t len, uint32_t mix, bool first_tile_of_grid) {
     // the bit tests here, per tile: hoisted out of the tile loop, hipcc kept each flag as a live
     // 64-bit mask and spilled SGPRs (the mixed-length kernel 24 against 14, C3 +1.1 us per launch)
     asm volatile("" : "+s"(report));
-    const bool mixed = mixed_tile && (!kMixedOnAsk || (report & kAskMixed) != 0u);
+    const bool mixed = mix != kMixNone && (!kMixedOnAsk || (report & kAskMixed) != 0u);
     const bool ran = first_tile_of_grid && (report & kAskRan) != 0u;
     const bool lng = (ran || report_watch(report)) && __ballot(len > kSmallMaxLen) != 0u;
-    return (mixed ? kPostMixed : 0u) | (ran ? (lng ? kPostRan | kPostRanLong : kPostRan) : (lng ? kPostLong : 0u));
+    return (mixed ? (mix == kMixGiant ? kPostMixed | kPostGiant : kPostMixed) : 0u) |
+           (ran ? (lng ? kPostRan | kPostRanLong : kPostRan) : (lng ? kPostLong : 0u));
 }
 __device__ __forceinline__ void post_tile(uint64_t report, uint32_t posts, uint32_t lane) {
     if (posts == 0u || lane != 0u) return;
-    if (posts & kPostMixed) post_report<kReportLatest>(report);
+    if (posts & kPostMixed) post_report<kReportLatest>(report, (posts & kPostGiant) ? kReportMixedGiant : 0u);
     if (posts & kPostRan) post_report<kReportRan>(report, (posts & kPostRanLong) ? kReportRanLong : 0u);
     if (posts & kPostLong) post_report<kReportLong>(report);
 }
@@ -1288,7 +1292,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
         for (int i = 0; i < kPfA; ++i) pf[i] = load_row(T.gfb, lpos(T.rel0 + kRowDwords * i, T.lo));
     }
     if (first) tile_geometry_a_tail<Lay::kCapBlocks>(T);
-    const uint32_t posts0 = first && report ? tile_posts<false>(report, T.len, mode_b_worthy(T.nd()), gwave == 0u) : 0u;
+    const uint32_t posts0 = first && report ? tile_posts<false>(report, T.len, mixed_class(T.nd()), gwave == 0u) : 0u;
     if (first) tile_header(T);
     FS_STAMP(13);
     FS_STAMP(9);
@@ -1435,7 +1439,7 @@ digest_kernel_a(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
                     pf[i] = load_row(T.gfb, i < T.H ? lpos(rel, T.lo) : rel);
                 }
             }
-            if (report) post_tile(report, tile_posts<false>(report, T.len, mode_b_worthy(T.nd()), false), lane);
+            if (report) post_tile(report, tile_posts<false>(report, T.len, mixed_class(T.nd()), false), lane);
             tile_header(T);
         }
     }
@@ -1502,7 +1506,8 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
     // is all the parse's vmcnt(kPrefetch) needs)
     if (first) prefetch_unit(U, pf);
     if (first) x4 = header_dma<false>(T, frames, lds, hw, gl0, lane);
-    const uint32_t posts0 = first && report ? tile_posts<true>(report, T.len, T.npass > 1, gwave == 0u) : 0u;
+    // (the mixed class only when the launch asks: a giant tile runs mode A here, so the pass count cannot tell)
+    const uint32_t posts0 = first && report ? tile_posts<true>(report, T.len, (report & kAskMixed) ? mixed_class(T.nd()) : kMixNone, gwave == 0u) : 0u;
     FS_STAMP(9);
     tables_landed<kPrefetch>(first, U.P > 0, x4);
     post_tile(report, posts0, lane);  // (after the counted wait, younger than the rows)
@@ -1656,7 +1661,8 @@ digest_kernel_ab(const uint8_t* __restrict__ frames, const uint64_t* __restrict_
             tile_geometry(T, U, tile, grp, gl, n, S, len, frames, lds, ws, fpt);
             header_dma<false>(T, frames, lds, hw, gl, lane);
             prefetch_unit(U, pf);
-            if (report) post_tile(report, tile_posts<true>(report, T.len, T.npass > 1, false), lane);
+            if (report)
+                post_tile(report, tile_posts<true>(report, T.len, (report & kAskMixed) ? mixed_class(T.nd()) : kMixNone, false), lane);
         }
     }
 }
@@ -1861,8 +1867,7 @@ digest_kernel_g(const uint8_t* __restrict__ frames, const uint64_t* __restrict__
     auto posts_of = [&](bool first_of_grid) __attribute__((always_inline)) -> uint32_t {
         const bool ask_mixed = (report & kAskMixed) != 0u;
         const int nd = G.len >= 4u ? G.ndall() : 0;
-        const bool mixed = ask_mixed && mode_b_worthy(nd);
-        return tile_posts<false>(report, G.len, mixed, first_of_grid);
+        return tile_posts<false>(report, G.len, ask_mixed ? mixed_class(nd) : kMixNone, first_of_grid);
     };
 
     // Preamble: the first tile's descriptors while the tables are built in place; geometry; the first
@@ -2271,9 +2276,10 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     const uint64_t rdev = reinterpret_cast<uint64_t>(report_dev);
     const bool can_report = report_host && rdev != 0u && (rdev & ~kReportAddrMask) == 0u;  // (64-B aligned too)
     uint64_t report = can_report ? rdev | ((uint64_t)id << 48) : 0u;
-    bool mixed = false;
+    bool mixed = false, giant = false;
     if (can_report) {
         const uint32_t latest = report_host[kReportLatest];
+        giant = (latest & kReportMixedGiant) != 0u;
         if (latest != report_host[kReportSeen]) {
             report_host[kReportSeen] = latest;
             report_host[kReportSeenSeq] = seq;
@@ -2295,7 +2301,8 @@ hipError_t launch_digest(const uint8_t* frames, const uint64_t* offsets, const u
     // segment kernel (digest_kernel_g: another mixed-length decomposition, slower on C3)
     if (force == 2 || force == 3 || force == 4) mixed = force != 4;
     if (force == kForceUniformHost) mixed = false;
-    const bool segments = force == 3;
+    // the automatic choice runs the segment kernel while the latest mixed report saw a giant tile
+    const bool segments = force == 3 || (mixed && giant && (force == 0 || force == kForceNoSmall || force == 8));
     // The small-frame kernel (RX digest and FCS verify; a TX fill keeps the 4-lane choice above).
     // The kernels report launches that met a frame longer than kSmallMaxLen (kReportLong), and the
     // 4-lane kernels, when asked (kAskRan), that a launch ran (kReportRan, with the grid's first

@@ -492,6 +492,33 @@ def test_auto_choice_first_launches():
         e.close()
 
 
+def test_auto_choice_giant_frames():
+    """Tiles that mix a 128-KB frame with 64-B frames: more pieces than the mixed-length kernel's mode B
+    covers (6 passes of 16), so it would stream the long frame with one group (~15x slower); the
+    kernels report such tiles (kReportMixedGiant) and the automatic choice moves to the segment kernel
+    (variant 3), which cuts any frame into equal chunks. Bit-exact before and after the switch; C3-like
+    traffic keeps the mixed-length kernel (test_auto_choice_first_launches)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(71)
+    ln = np.tile(np.array([131072] + [64] * 15, dtype=np.int32), 256)
+    off = np.zeros(len(ln), np.int64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.int64))
+    buf = rng.integers(0, 256, int(off[-1] + ln[-1] + 64), dtype=np.uint8)
+    e = Engine(0)
+    try:
+        check(e, buf, off, ln, label="giant mix, first launch")
+        kinds = []
+        for _ in range(40):
+            run_device(e, buf, off, ln)
+            kinds.append(e.last_kernel())
+        assert kinds[-1] == Engine.KERNEL_SEGMENTS, kinds
+        check(e, buf, off, ln, label="giant mix, segment kernel")
+        assert e.last_kernel() == Engine.KERNEL_SEGMENTS
+    finally:
+        e.close()
+
+
 def test_host_first_call_kernel_choice():
     """a fresh context's FIRST host-staged call (what a short-lived Go
     RecvEthBatch context makes) runs the one-pass kernel when the batch's lengths lie within 256 B of
