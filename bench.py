@@ -129,6 +129,9 @@ class GpuOps:
 GPU = GpuOps()
 
 
+KERNEL_NAMES = {2: "digest_kernel_ab", 3: "digest_kernel_g", 4: "digest_kernel_a", 8: "digest_kernel_s"}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -164,7 +167,7 @@ def parse():
                         "launches run first, over the streams, without the gather (reported as prewarm_launches)")
     p.add_argument("--kernel", type=int, default=None,
                    help="fs_ctx_set_kernel variant: 0 automatic (default; short-frame traffic moves it to the "
-                        "small-frame kernel), 2 mixed-length, 4 one-pass, 8 small-frame preferred")
+                        "small-frame kernel), 2 mixed-length, 3 segment, 4 one-pass, 8 small-frame preferred")
     p.add_argument("--workgroups", type=int, default=0,
                    help="fs_ctx_set_workgroups: workgroups per launch (0: one per CU; fewer give each wave several "
                         "tiles and let consecutive launches run side by side)")
@@ -603,12 +606,14 @@ def main():
                                 "the line two neighbouring frames share is fetched twice (~8.4% on C2); "
                                 "traffic_calibrated divides that pattern factor out (the kernel's excess beyond it)"
                 if traffic is not None else None,
-                "kernel": {0: "automatic: digest_kernel_a (one-pass) for uniform batches, digest_kernel_ab for mixed, "
+                "kernel": {0: "automatic: digest_kernel_a (one-pass) for uniform batches, digest_kernel_ab for mixed "
+                              "(digest_kernel_g when a mixed tile holds a frame beyond its pieces), "
                               "digest_kernel_s once the launches it has seen ran had no frame over 128 B",
-                           2: "digest_kernel_ab (mixed-length)", 4: "digest_kernel_a (one-pass)",
+                           2: "digest_kernel_ab (mixed-length)", 3: "digest_kernel_g (segments)",
+                           4: "digest_kernel_a (one-pass)",
                            8: "digest_kernel_s preferred (fs_ctx_set_kernel 8: until a launch meets a frame over 128 B, "
                               "then the automatic choice until short traffic resumes)"}.get(args.kernel),
-                "kernel_chosen": {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine_last_kernel),
+                "kernel_chosen": KERNEL_NAMES.get(engine_last_kernel),
                 "kernel_avg_us": round(k_avg_ms * 1e3, 3),
                 "kernel_timing": "HIP events around K back-to-back launches on the launch stream",
                 "algorithmic_bytes_per_launch": bytes_per_batch,
@@ -729,7 +734,7 @@ def sub_record_c3(args, dev):
         batches.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)))
     nbytes = int(batches[0][2].sum().item())
     elapsed, k_ms = single_gpu_region(engine, batches, args.steps, args.warmup, args.min_warm, max(1, args.streams), dev)
-    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine.last_kernel())
+    chosen = KERNEL_NAMES.get(engine.last_kernel())
     engine.close()
     del batches
     return {
@@ -766,7 +771,7 @@ def sub_record_small(args, dev):
         batches.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)))
     nbytes = int(batches[0][2].sum().item())
     elapsed, k_ms = single_gpu_region(engine, batches, args.steps, args.warmup, args.min_warm, max(1, args.streams), dev)
-    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine.last_kernel())
+    chosen = KERNEL_NAMES.get(engine.last_kernel())
     engine.close()
     del batches
     return {
@@ -807,7 +812,7 @@ def sub_record_op(args, dev, op: str):
     nbytes = int(batches[0][2].sum().item())
     elapsed, k_ms = single_gpu_region(engine, batches, args.steps, args.warmup, args.min_warm, max(1, args.streams), dev,
                                       op=op, flags=3)
-    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(engine.last_kernel())
+    chosen = KERNEL_NAMES.get(engine.last_kernel())
     # the results of the last launches: every frame filled / verified
     GPU.sync()
     engine.close()
@@ -871,7 +876,7 @@ def sub_record_small_host(args):
         res[name] = time.perf_counter() - t0
         gc.enable()
     assert np.array_equal(out, pout) and np.array_equal(st, pst)
-    chosen = {2: "digest_kernel_ab", 4: "digest_kernel_a", 8: "digest_kernel_s"}.get(eng.last_kernel())
+    chosen = KERNEL_NAMES.get(eng.last_kernel())
     eng.close()
     el = res["pageable_results"]
     cpu = cpu_baseline("small", 4.0, args.cpu_threads) if args.cpu_seconds > 0 else None

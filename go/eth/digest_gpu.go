@@ -101,12 +101,13 @@ func (g *GPU) lastErr() error { return errors.New("framesum: " + C.GoString(C.fs
 
 // Kernel variants of fs_ctx_set_kernel (include/framesum.h): results never depend on them.
 const (
-	KernelAuto    = 0 // one-pass kernel for uniform lengths, piece-splitting kernel for mixed ones, the
+	KernelAuto     = 0 // one-pass kernel for uniform lengths, piece-splitting (or segment) kernel for mixed ones, the
 	// one-lane-per-frame kernel once the launches seen have had no frame over 128 B;
 	// DigestBatch picks the one-lane-per-frame kernel itself for a batch of frames all <= 128 B
-	KernelMixed   = 2 // piece-splitting kernel
-	KernelOnePass = 4 // one-pass kernel
-	KernelSmall   = 8 // one lane per frame preferred, until a launch reports a frame over 128 B: a
+	KernelMixed    = 2 // piece-splitting kernel
+	KernelSegments = 3 // equal chunks per frame: tiles that mix a giant frame (beyond the pieces) with short ones
+	KernelOnePass  = 4 // one-pass kernel
+	KernelSmall    = 8 // one lane per frame preferred, until a launch reports a frame over 128 B: a
 	// stack whose traffic is short frames (ACKs, DNS, DHCP, the reference's 47-byte benchmark
 	// frames in stacks/benchmark_test.go)
 )

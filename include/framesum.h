@@ -226,33 +226,38 @@ uint64_t fs_shard_slab_bytes(uint64_t n, uint32_t nshards);
 fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards, uint64_t n, fs_digest* out,
                           uint8_t* status, void* stream);
 
-/* Kernel variant of a context's launches. The engine has three kernels: a one-pass kernel for
+/* Kernel variant of a context's launches. The engine has four kernels: a one-pass kernel for
  * batches of similar frame lengths (each frame read as the 64-byte blocks that hold it), a
  * mixed-length kernel that splits long frames into 768-byte pieces when a tile of 16 frames mixes
- * very different lengths, and a small-frame kernel (one lane per frame, small workgroups) for
- * traffic of short frames such as the reference's 47-byte benchmark frames. The kernels report
- * whether a launch's batch had mixed-length tiles and whether it had a frame longer than 128 bytes
- * (sampled on steady traffic: each report is a store to host memory); the host reads those reports
- * a few launches late.
- *   0 (default): automatic. Mixed-length tiles select the mixed-length kernel, similar lengths the
- *     one-pass kernel; after 16 launches seen to run with no frame over 128 bytes, the small-frame
- *     kernel, until a launch reports a longer frame.
- *   2 / 4: always the mixed-length / the one-pass kernel.
+ * very different lengths, a segment kernel that cuts every frame of such a tile into equal chunks
+ * (for tiles whose longest frame is beyond the pieces' reach, e.g. a 128-KB frame among 64-byte
+ * ones), and a small-frame kernel (one lane per frame, small workgroups) for traffic of short
+ * frames such as the reference's 47-byte benchmark frames. The kernels report whether a launch's
+ * batch had mixed-length tiles (and whether one of them held such a giant frame) and whether it had
+ * a frame longer than 128 bytes (sampled on steady traffic: each report is a store to host memory);
+ * the host reads those reports a few launches late.
+ *   0 (default): automatic. Mixed-length tiles select the mixed-length kernel (the segment kernel
+ *     when the report says giant), similar lengths the one-pass kernel; after 16 launches seen to
+ *     run with no frame over 128 bytes, the small-frame kernel, until a launch reports a longer frame.
+ *   2 / 3 / 4: always the mixed-length / the segment / the one-pass kernel.
  *   8: the small-frame kernel preferred: it runs until a launch reports a frame over 128 bytes,
- *     then the automatic choice between the other two until 2 launches have run short again.
+ *     then the automatic choice among the others until 2 launches have run short again.
  * The host-staged calls see every length: with 0 or 8 a batch whose frames are all <= 128 bytes
- * runs the small-frame kernel, any other batch the automatic choice. A TX fill never runs the
- * small-frame kernel. Because reports arrive late, a launch of the small-frame kernel can still meet
- * long frames: they stay correct there but one lane streams each of them (hundreds of us for a
- * batch of jumbo frames). Any other variant is FS_E_INVALID. Results are identical in every case;
- * only the speed differs. */
+ * runs the small-frame kernel; with 0 a batch whose lengths all lie within 256 bytes of each other
+ * runs the one-pass kernel from the context's first call; any other batch the automatic choice. A
+ * TX fill never runs the small-frame kernel, and the in-place host call never the segment kernel.
+ * Because reports arrive late, a launch of the small-frame kernel can still meet long frames: they
+ * stay correct there but one lane streams each of them (hundreds of us for a batch of jumbo
+ * frames). Any other variant is FS_E_INVALID. Results are identical in every case; only the speed
+ * differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
-/* The kernel (2 mixed-length, 4 one-pass, 8 small-frame) the context's latest launch ran; 0 before
- * its first launch, FS_E_INVALID for a null context. With variant 0 a context's first 16 launches
- * run the mixed-length kernel (2), which keeps itself chosen while it meets mixed tiles; uniform
- * traffic then moves to the one-pass kernel (4), and traffic of frames <= 128 bytes to the
- * small-frame kernel (8). */
+/* The kernel (2 mixed-length, 3 segment, 4 one-pass, 8 small-frame) the context's latest launch
+ * ran; 0 before its first launch, FS_E_INVALID for a null context. With variant 0 a context's first
+ * 16 device-resident launches run the mixed-length kernel (2), which keeps itself chosen while it
+ * meets mixed tiles (moving to the segment kernel, 3, when they hold giant frames); uniform traffic
+ * then moves to the one-pass kernel (4), and traffic of frames <= 128 bytes to the small-frame
+ * kernel (8). */
 int fs_ctx_last_kernel(const fs_ctx* ctx);
 
 /* Workgroups per launch of a context's kernels: 0 (the default) launches one 16-wave

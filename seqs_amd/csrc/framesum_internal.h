@@ -44,8 +44,9 @@ void build_tables(FsTables* t);
 // host-mapped word: a kernel writes its launch id there when its batch has tiles of widely
 // mixed frame lengths; launches within a window after such a report use the kernel variant
 // that can split long frames into pieces (mode B), others the leaner one-pass variant. The choice never changes a
-// result, only the speed. `force`: 0 = that choice, 2 = always the mixed-length kernel, 4 = always
-// the one-pass kernel (fs_ctx_set_kernel; tests run every case through both). `next_id`: the
+// result, only the speed. `force`: 0 = that choice, 2 / 3 / 4 / 8 = always the mixed-length / segment /
+// one-pass kernel, the small-frame kernel preferred (fs_ctx_set_kernel; tests run every case through
+// each), or one of the host-staged path's kForce* values below. `next_id`: the
 // context's launch counter (the ids its launches report under).
 // `op`: the RX digest; the TX fill (`wframes` = the same frames, writable; `tx` = FS_FILL_* flags:
 // checksums written into the frames and/or the FCS appended after them); or the RX digest of

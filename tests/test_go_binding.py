@@ -46,7 +46,7 @@ def test_go_files_declare_the_binding():
     assert go == c
     # the Go kernel-variant constants are the values fs_ctx_set_kernel accepts
     kv = {int(v) for v in re.findall(r"Kernel[A-Za-z]+\s+= (\d+)", eth)}
-    assert kv == {0, 2, 4, 8}
+    assert kv == {0, 2, 3, 4, 8}
 
 
 def write_list(path, frames):
