@@ -245,11 +245,10 @@ fs_status fs_deinterleave(fs_ctx* ctx, const uint8_t* gathered, uint32_t nshards
  * The host-staged calls see every length: with 0 or 8 a batch whose frames are all <= 128 bytes
  * runs the small-frame kernel; with 0 a batch whose lengths all lie within 256 bytes of each other
  * runs the one-pass kernel from the context's first call; any other batch the automatic choice. A
- * TX fill never runs the small-frame kernel, and the in-place host call never the segment kernel.
- * Because reports arrive late, a launch of the small-frame kernel can still meet long frames: they
- * stay correct there but one lane streams each of them (hundreds of us for a batch of jumbo
- * frames). Any other variant is FS_E_INVALID. Results are identical in every case; only the speed
- * differs. */
+ * TX fill never runs the small-frame kernel. Because reports arrive late, a launch of the
+ * small-frame kernel can still meet long frames: they stay correct there but one lane streams each
+ * of them (hundreds of us for a batch of jumbo frames). Any other variant is FS_E_INVALID. Results
+ * are identical in every case; only the speed differs. */
 fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
 
 /* The kernel (2 mixed-length, 3 segment, 4 one-pass, 8 small-frame) the context's latest launch
