@@ -779,6 +779,23 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    // `conc`: the one-pass kernel's pattern (4 lanes per frame, block-aligned whole blocks) with fewer
+    // frames streaming chip-wide at once: W waves per CU (one workgroup per CU), each wave taking
+    // 16 / W... tiles one after another (tile k of wave w = w + k * nwaves: at any time the chip
+    // streams a window of the batch, not all of it) through one continuous ring of PF rows
+    if (argc > 1 && std::string(argv[1]) == "conc") {
+        for (int rep = 0; rep < 2; ++rep) {
+            STREAM(4, 16, 1);
+            TILES(4, 5, 2, 16);
+            TILES(4, 10, 2, 8);
+            TILES(4, 12, 2, 8);
+            TILES(4, 16, 2, 8);
+            TILES(4, 16, 2, 4);
+            TILES(4, 24, 2, 4);
+            TILESX(4, 5, 2, 8, 2);
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "span16") {
         uint2* part;
         const uint32_t nspans = (nf + 15) / 16;
