@@ -620,6 +620,54 @@ __global__ void __launch_bounds__(1024) k_span16(const uint8_t* __restrict__ bas
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// `proxy` (round 6): the one-pass kernel's shape with its preamble and row work, to compare one
+// 16-wave workgroup per CU (152 KB of LDS) with two 8-wave workgroups (80 KB each) when launches
+// overlap. Preamble: a dependent descriptor load per lane (the frame base), the LDS image built by
+// VALU + ds_write (LDSB bytes per workgroup) while it flies, the first PF rows issued, a barrier.
+// Rows: 4 lanes per frame, block-aligned whole 64-B blocks (the C2 geometry), per row 16 lookups per
+// lane into a 64-KB region-A-like table at its 256-B entry stride (lane-dependent slot: conflict-free)
+// and the XORs. Tables hold junk; results are not checked.
+template <int WPB, int PF>
+__global__ void __launch_bounds__(64 * WPB) k_proxy(const uint8_t* __restrict__ base, const uint32_t* __restrict__ desc,
+                                                    uint32_t nframes, uint32_t flen, uint32_t ldsb, uint32_t* out) {
+    extern __shared__ __attribute__((aligned(16))) char dl[];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, grp = lane >> 2, gl = lane & 3u;
+    const uint32_t gwave = wave * gridDim.x + blockIdx.x;
+    const uint32_t f = gwave * 16u + grp;
+    const uint32_t d = desc[f < nframes ? f : 0u];  // the descriptor round trip
+    for (uint32_t o = threadIdx.x * 16u; o < ldsb; o += 64u * WPB * 16u)
+        *reinterpret_cast<u32x4*>(dl + o) = u32x4{o * 0x9E3779B1u, o ^ 0x5bd1e995u, o * 7u, ~o};
+    const uint64_t S = (uint64_t)(f < nframes ? f : 0u) * flen + d;
+    const uint64_t b0 = S / 64, b1 = (S + flen - 1) / 64;
+    const int rows = (int)(b1 - b0 + 1);
+    const uint8_t* fb = base + b0 * 64 + 16u * gl;
+    u32x4 pf[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) pf[i] = *reinterpret_cast<const u32x4_a4*>(fb + 64 * min(i, rows - 1));
+    __syncthreads();
+    const uint32_t c = lane & 7u;
+    uint32_t A[4] = {0u, 0u, 0u, 0u};
+    for (int r0 = 0; r0 < rows; r0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const uint32_t w[4] = {pf[i].x, pf[i].y, pf[i].z, pf[i].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t a = A[j];
+                uint32_t t = w[j];
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    t ^= *reinterpret_cast<const uint32_t*>(dl + (((a >> (8 * b)) & 0xffu) << 8) + 32u * b + 4u * c);
+                A[j] = t;
+            }
+            const int rn = r0 + i + PF;
+            pf[i] = *reinterpret_cast<const u32x4_a4*>(fb + 64 * min(rn, rows - 1));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if ((A[0] ^ A[1] ^ A[2] ^ A[3]) == 0x12345678u) out[0] = 1u;
+}
+
 int main(int argc, char** argv) {
     // `dir [flen]`: forward-only (AL 2) against alternating-direction (AL 3) whole blocks
     const bool dir = argc > 1 && std::string(argv[1]).rfind("dir", 0) == 0;
@@ -783,6 +831,44 @@ int main(int argc, char** argv) {
     // frames streaming chip-wide at once: W waves per CU (one workgroup per CU), each wave taking
     // 16 / W... tiles one after another (tile k of wave w = w + k * nwaves: at any time the chip
     // streams a window of the batch, not all of it) through one continuous ring of PF rows
+    if (argc > 1 && std::string(argv[1]) == "proxy") {
+        uint32_t* desc;
+        CHECK(hipMalloc(&desc, (size_t)nf * 4));
+        CHECK(hipMemset(desc, 0, (size_t)nf * 4));
+        CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_proxy<16, 5>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_proxy<8, 5>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        auto prox = [&](int wpb, uint32_t ldsb, const char* name) {
+            double res[3];
+            int k = 0;
+            for (int ns : {1, 4, 5}) {
+                for (int pass = 0; pass < 2; ++pass) {
+                    CHECK(hipDeviceSynchronize());
+                    auto t0 = std::chrono::steady_clock::now();
+                    for (int i = 0; i < reps; ++i) {
+                        if (wpb == 16)
+                            hipLaunchKernelGGL((k_proxy<16, 5>), dim3(cus), dim3(1024), ldsb, st[i % ns], bufs[i % NB], desc,
+                                               nf, flen, ldsb, out);
+                        else
+                            hipLaunchKernelGGL((k_proxy<8, 5>), dim3(cus * 2), dim3(512), ldsb, st[i % ns], bufs[i % NB],
+                                               desc, nf, flen, ldsb, out);
+                    }
+                    CHECK(hipDeviceSynchronize());
+                    res[k] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+                }
+                ++k;
+            }
+            printf("%-40s 1 stream %8.2f us | 4 streams %8.2f us | 5 streams %8.2f us\n", name, res[0], res[1], res[2]);
+        };
+        for (int rep = 0; rep < 2; ++rep) {
+            prox(16, 152 * 1024, "proxy 16 waves, 152 KB, 1 WG/CU");
+            prox(8, 80 * 1024, "proxy 8 waves, 80 KB, 2 WG/CU");
+            prox(8, 96 * 1024, "proxy 8 waves, 96 KB (1 WG/CU)");
+            prox(16, 64 * 1024, "proxy 16 waves, 64 KB, 1 WG/CU (build)");
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "conc") {
         for (int rep = 0; rep < 2; ++rep) {
             STREAM(4, 16, 1);
