@@ -492,6 +492,34 @@ def test_auto_choice_first_launches():
         e.close()
 
 
+@pytest.mark.parametrize("seed", [81, 82])
+def test_random_giant_mix(engine, seed):
+    """Tiles mixing frames beyond mode B's reach (60 KB .. 400 KB: valid TCP/UDP frames up to IP's
+    64-KB TotalLength, random bytes past it) with short and MTU frames, at every byte alignment:
+    whatever kernel the column runs (the segment kernel's chunks cut them into up to 16 segments,
+    the piece kernel falls back to one group per frame), bit-exact against the oracle."""
+    import random
+
+    import framegen
+    rnd = random.Random(seed)
+    frames = []
+    for _ in range(48):  # 48 tiles of 16 frames
+        tile = []
+        for _ in range(rnd.choice([1, 1, 2, 3])):
+            if rnd.random() < 0.5:
+                tile.append(framegen.valid_frame(rnd, proto=rnd.choice([6, 17]), payload=rnd.randrange(60000, 65400)))
+            else:
+                tile.append(rnd.randbytes(rnd.randrange(65536, 400000)))
+        while len(tile) < 16:
+            r = rnd.random()
+            tile.append(framegen.valid_frame(rnd, proto=rnd.choice([6, 17]),
+                                             payload=rnd.randrange(0, 40) if r < 0.5 else rnd.randrange(400, 1446)))
+        rnd.shuffle(tile)
+        frames.extend(tile)
+    buf, off, ln = pack_frames(frames, align=1)
+    check(engine, buf, off, ln, label=f"random giant mix {seed}")
+
+
 def test_auto_choice_giant_frames():
     """Tiles that mix a 128-KB frame with 64-B frames: more pieces than the mixed-length kernel's mode B
     covers (6 passes of 16), so it would stream the long frame with one group (~15x slower); the
