@@ -256,7 +256,10 @@ fs_status fs_ctx_set_kernel(fs_ctx* ctx, int variant);
  * 16 device-resident launches run the mixed-length kernel (2), which keeps itself chosen while it
  * meets mixed tiles (moving to the segment kernel, 3, when they hold giant frames); uniform traffic
  * then moves to the one-pass kernel (4), and traffic of frames <= 128 bytes to the small-frame
- * kernel (8). */
+ * kernel (8). The window costs uniform 1500-byte traffic about 1.5 us per launch (~23 us once per
+ * context, measured on MI355X); mixed traffic it saves ~80 us per launch. A caller that knows its
+ * device-resident traffic is uniform can set variant 4 (host-staged calls see the lengths and skip
+ * the window for uniform batches by themselves). */
 int fs_ctx_last_kernel(const fs_ctx* ctx);
 
 /* Workgroups per launch of a context's kernels: 0 (the default) launches one 16-wave
